@@ -1,0 +1,154 @@
+/*
+ * pixpath.h -- C ABI of libpixpath.so, the MI355X (gfx950) raw-frame pixel path
+ * behind pnats2avhd/processing-chain's command builders (lib/ffmpeg.py) and SRC
+ * analysis hooks (util/SRC_analysis.py, util/complexity_classification.py).
+ *
+ * Plain C types only: device pointers, byte strides, sizes, an opaque context.
+ * Every entry point returns PP_OK (0) or a negative PP_ERR_* code; the message
+ * of the last failure is available from pp_last_error() (thread-local).
+ * Kernels are enqueued on the caller's HIP stream (`stream`, a hipStream_t
+ * passed as void*; NULL = the null stream) and never synchronise it.
+ * A context is bound to one device and is not thread-safe (one per process,
+ * matching the one-process-per-GPU model of SURVEY.md section 8e).
+ *
+ * Which reference interface each entry point replaces is given per function as
+ * reference file:line.  The reference reaches all of these through ffmpeg
+ * command strings; the strings are reproduced by the Python host
+ * (processing-chain_amd/pixpath/ffmpeg.py), which calls this library.
+ */
+#ifndef PIXPATH_H
+#define PIXPATH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PP_ABI_VERSION 1
+
+/* return codes */
+#define PP_OK 0
+#define PP_ERR_INVALID -1     /* bad argument / unsupported combination */
+#define PP_ERR_HIP -2         /* HIP runtime failure */
+#define PP_ERR_NOMEM -3
+#define PP_ERR_UNSUPPORTED -4
+
+/* pixel formats (ffmpeg -pix_fmt names in comments) */
+enum pp_pix_fmt {
+    PP_FMT_YUV420P = 0,      /* yuv420p */
+    PP_FMT_YUV422P = 1,      /* yuv422p */
+    PP_FMT_YUV444P = 2,      /* yuv444p */
+    PP_FMT_YUV420P10LE = 3,  /* yuv420p10le */
+    PP_FMT_YUV422P10LE = 4,  /* yuv422p10le */
+    PP_FMT_YUV444P10LE = 5,  /* yuv444p10le */
+    PP_FMT_UYVY422 = 6,      /* uyvy422 (packed, 1 plane) */
+    PP_FMT_V210 = 7          /* -c:v v210 payload (packed, 1 plane) */
+};
+
+/* swscale flag values (same bits as FFmpeg's SWS_*) */
+#define PP_SWS_BILINEAR 0x2
+#define PP_SWS_BICUBIC 0x4
+#define PP_SWS_LANCZOS 0x200
+#define PP_SWS_PARAM_DEFAULT 123456.0
+
+/*
+ * A batch of `nframes` frames.  Plane p of frame f starts at
+ * data[p] + f * frame_stride[p]; rows are linesize[p] bytes apart.
+ * Packed formats use plane 0 only.
+ */
+typedef struct pp_frames {
+    void *data[3];
+    int64_t linesize[3];
+    int64_t frame_stride[3];
+} pp_frames;
+
+typedef struct pp_ctx pp_ctx;
+typedef struct pp_scale_plan pp_scale_plan;
+
+/* ---- library / context ------------------------------------------------- */
+int pp_abi_version(void);
+const char *pp_last_error(void);
+/* Select `device` and create a context.  Replaces nothing in the reference
+ * (the reference runs CPU processes, lib/cmd_utils.py:93-101). */
+int pp_ctx_create(int device, pp_ctx **out);
+int pp_ctx_destroy(pp_ctx *ctx);
+
+/* Byte size of one plane of one frame and the v210 line size (v210enc.c:
+ * ceil(w/48)*48*8/3). */
+int64_t pp_plane_bytes(int fmt, int w, int h, int plane, int64_t linesize);
+int64_t pp_v210_linesize(int w);
+
+/* ---- scaling / format conversion (libswscale restatement) --------------
+ * Replaces `scale=W:H:flags=bicubic` at lib/ffmpeg.py:992 (create_avpvs_short),
+ * :1038 (create_avpvs_segment), :1213 (create_cpvs mobile), `scale=W:-2` at
+ * :800 (encode_segment) and the implicit `-pix_fmt` conversions at :994, :1048,
+ * :1198.  flags: PP_SWS_BICUBIC | PP_SWS_LANCZOS | PP_SWS_BILINEAR; param0/1 as
+ * FFmpeg's sws param[0]/[1] (PP_SWS_PARAM_DEFAULT = FFmpeg default).
+ * dst_fmt may be planar YUV or PP_FMT_UYVY422 (packed output path).
+ * Coefficient tables are built on the host once per plan and kept in HBM.
+ * ctx == NULL builds a host-only plan (filter introspection, no execution). */
+int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int src_w, int src_h,
+                         int dst_fmt, int dst_w, int dst_h, int flags,
+                         double param0, double param1, pp_scale_plan **out);
+int pp_scale_plan_destroy(pp_scale_plan *plan);
+/* Introspection for parity tests: which = 0 luma-H, 1 chroma-H, 2 luma-V,
+ * 3 chroma-V.  Copies the FFmpeg-layout filter (before device compaction):
+ * coef[n * size] int16, pos[n] int32 on the host.  Returns size (>0),
+ * 0 when the plan uses an unscaled converter, or <0. */
+int pp_scale_plan_filter(const pp_scale_plan *plan, int which, int16_t *coef,
+                         int32_t *pos, int capacity);
+/* Run the plan on `nframes` device frames. */
+int pp_scale_execute(pp_scale_plan *plan, const pp_frames *src,
+                     const pp_frames *dst, int nframes, void *stream);
+
+/* ---- padding -----------------------------------------------------------
+ * Replaces `pad=width=DW:height=DH:x=(ow-iw)/2:y=(oh-ih)/2` at
+ * lib/ffmpeg.py:1183 (create_cpvs PC) and :1209 (tablet).  Black is
+ * Y 16 / C 128 scaled to the bit depth; x/y are rounded down to the chroma
+ * grid.  Pass x = y = -1 for the reference's centring expression. */
+int pp_pad_execute(pp_ctx *ctx, int fmt, int src_w, int src_h,
+                   const pp_frames *src, int dst_w, int dst_h, int x, int y,
+                   const pp_frames *dst, int nframes, void *stream);
+
+/* ---- CPVS packers ------------------------------------------------------
+ * `-c:v v210 -pix_fmt yuv422p10le` (lib/test_config.py:208-215 via
+ * lib/ffmpeg.py:1198): pack yuv422p10le into v210 (libavcodec/v210enc.c);
+ * dst plane 0 with linesize >= pp_v210_linesize(w). */
+int pp_v210_pack(pp_ctx *ctx, int w, int h, const pp_frames *src,
+                 const pp_frames *dst, int nframes, void *stream);
+
+/* ---- stall compositing (spec PP-STALL-1) -----------------
+ * Replaces the external `bufferer -s spinner.png` call at
+ * p03_generateAvPvs.py:236-243.  Uploads one spinner animation (n RGBA8
+ * frames of sw x sh, host memory) converted for `fmt`. */
+int pp_spinner_upload(pp_ctx *ctx, int fmt, const uint8_t *rgba, int n,
+                      int sw, int sh);
+/* For each output frame k: dst[k] = src[src_index[k]] (or black when
+ * src_index[k] < 0) with spinner frame spinner_index[k] composited centred
+ * (no overlay when spinner_index[k] < 0).  Index arrays are host memory. */
+int pp_stall_compose(pp_ctx *ctx, int fmt, int w, int h, const pp_frames *src,
+                     const int32_t *src_index, const int32_t *spinner_index,
+                     const pp_frames *dst, int nframes, void *stream);
+
+/* ---- P.910 SI/TI (spec PP-SITI-1) ------------------------
+ * New feature behind util/SRC_analysis.py:120-147 (analyse_src) and
+ * util/complexity_classification.py:50-69 (get_difficulty).
+ * luma: nframes frames of w x h, 8- or 10-bit (uint16 LE), linesize and
+ * frame_stride in bytes.  prev: the frame before luma[0] (1-frame halo) or
+ * NULL.  si/ti: DEVICE arrays of nframes doubles; ti[0] is NaN without prev. */
+int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma,
+            int64_t linesize, int64_t frame_stride, int nframes,
+            const void *prev, double *si, double *ti, void *stream);
+
+/* ---- host helpers --------------------------------------------------------
+ * vf_fps output->input frame map (lib/ffmpeg.py:832-834, :959-961, :1038,
+ * :1179): map[k] = input frame shown at output frame k.  Returns the number of
+ * output frames (<= capacity) or <0. */
+int pp_fps_map(int n_in, int64_t in_num, int64_t in_den, int64_t out_num,
+               int64_t out_den, int32_t *map, int capacity);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PIXPATH_H */

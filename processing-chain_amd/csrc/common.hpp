@@ -1,0 +1,66 @@
+// Shared host-side helpers of libpixpath.so: error reporting, pixel-format
+// table, the context object.  See include/pixpath.h for the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/pixpath.h"
+
+namespace pp {
+
+void set_error(const char *fmt, ...);
+
+#define PP_FAIL(code, ...)                 \
+    do {                                   \
+        ::pp::set_error(__VA_ARGS__);      \
+        return (code);                     \
+    } while (0)
+
+#define PP_HIP(expr)                                                              \
+    do {                                                                          \
+        hipError_t e_ = (expr);                                                   \
+        if (e_ != hipSuccess)                                                     \
+            PP_FAIL(PP_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));  \
+    } while (0)
+
+// Planar layout of a format: bit depth, chroma subsampling, plane count.
+struct FmtInfo {
+    int depth;   // bits per sample
+    int hsub;    // log2 horizontal chroma subsampling
+    int vsub;    // log2 vertical chroma subsampling
+    bool packed; // uyvy422 / v210
+    bool valid;
+};
+
+inline FmtInfo fmt_info(int f) {
+    switch (f) {
+    case PP_FMT_YUV420P: return {8, 1, 1, false, true};
+    case PP_FMT_YUV422P: return {8, 1, 0, false, true};
+    case PP_FMT_YUV444P: return {8, 0, 0, false, true};
+    case PP_FMT_YUV420P10LE: return {10, 1, 1, false, true};
+    case PP_FMT_YUV422P10LE: return {10, 1, 0, false, true};
+    case PP_FMT_YUV444P10LE: return {10, 0, 0, false, true};
+    case PP_FMT_UYVY422: return {8, 1, 0, true, true};
+    case PP_FMT_V210: return {10, 1, 0, true, true};
+    default: return {0, 0, 0, false, false};
+    }
+}
+
+inline int ceil_rshift(int a, int s) { return -((-a) >> s); }
+
+struct Ctx {
+    int device = 0;
+    // spinner animation (PP-STALL-1), device resident
+    int spin_fmt = -1, spin_n = 0, spin_w = 0, spin_h = 0;
+    void *spin_buf = nullptr; // [n][Y(w*h) A(w*h) U V Ac (cw*ch each)] uint16
+};
+
+} // namespace pp
+
+struct pp_ctx : pp::Ctx {};

@@ -1,0 +1,620 @@
+// Scaler plans and the fused separable polyphase kernel (gfx950).
+//
+// Reference semantics: FFmpeg 7.0 libswscale generic path as used by
+// `scale=W:H:flags=bicubic` (lib/ffmpeg.py:992, :1038, :1213, :800) and the
+// implicit `-pix_fmt` conversions (:994, :1048, :1198):
+//   hScale{8,16}To15   -> 15-bit intermediates  (Σ src*hcoef) >> (8-bit: 7, N-bit: N-1), min 32767
+//   yuv2planeX_8       -> clip_u8((dither<<12 + Σ inter*vcoef) >> 19)
+//   yuv2planeX_10      -> clip_u10((1<<16 + Σ inter*vcoef) >> 17)
+// dither = ff_dither_8x8_128[row & 7][(col + off) & 7] when a >8-bit source is
+// narrowed to 8 bit (off = 3 for the V plane), flat 64 otherwise.
+//
+// MI355X design: one workgroup (256 lanes = 4 wave64) owns a 256-wide x TH-tall
+// output tile of one plane of one frame.  It stages the source window
+// (R rows x S cols, 16-B vector loads) in LDS, runs the horizontal pass
+// LDS->LDS (15-bit int16 intermediates, coefficients in VGPRs, one output
+// column per lane), then the vertical pass LDS->HBM with wave-uniform
+// coefficients (scalar loads) and 4 outputs per lane (ds_read_b64 of 4
+// intermediates per tap).  Intermediates never touch HBM: traffic is one read
+// of the source (+ L2-served halo rows) and one write of the output.
+// All three planes of a whole frame batch go in ONE launch
+// (blockIdx.x = tile over the planes, blockIdx.y = frame).
+#include <algorithm>
+#include <cstring>
+#include <memory>
+
+#include "common.hpp"
+#include "filters.hpp"
+
+namespace pp {
+
+constexpr int kTileW = 256;      // output columns per workgroup
+constexpr int kThreads = 256;    // 4 waves
+constexpr int kLdsBudget = 40 * 1024;
+
+__constant__ uint8_t c_dither[8][8] = {
+    {36, 68, 60, 92, 34, 66, 58, 90},  {100, 4, 124, 28, 98, 2, 122, 26},
+    {52, 84, 44, 76, 50, 82, 42, 74},  {116, 20, 108, 12, 114, 18, 106, 10},
+    {32, 64, 56, 88, 38, 70, 62, 94},  {96, 0, 120, 24, 102, 6, 126, 30},
+    {48, 80, 40, 72, 54, 86, 46, 78},  {112, 16, 104, 8, 118, 22, 110, 14},
+};
+
+struct PlaneJob {
+    int sw, sh, dw, dh;
+    int tiles_x, tiles_y, tile_base, th;
+    int vt, R, S;         // V taps, staged rows / cols (max over tiles)
+    int dither_off;       // 0 (Y, U) or 3 (V)
+    const int32_t *hpos;  // [dw]   window start (absolute source column)
+    const int16_t *hcoef; // [dw * HT]
+    const int32_t *vpos;  // [dh]
+    const int16_t *vcoef; // [dh * vt]
+    const int32_t *tile_c0, *tile_cn; // [tiles_x] staged column window
+    const int32_t *tile_r0, *tile_rn; // [tiles_y] staged row window
+};
+
+struct ScaleArgs {
+    PlaneJob pl[3];
+    const uint8_t *src[3];
+    int64_t sls[3], sfs[3];
+    uint8_t *dst[3];
+    int64_t dls[3], dfs[3];
+    int nplanes;
+    int hshift;   // 7 for 8-bit sources, depth-1 otherwise
+    int dither;   // ordered dither (>8-bit source narrowed to 8 bit)
+    int vec_src;  // all source rows 16-B aligned
+    int vec_dst;  // all destination rows 8-B aligned (4 outputs per lane)
+};
+
+template <typename ST>
+__device__ inline void stage_chunk(uint16_t *lds_dst, const ST *g, int col, int sw, bool vec) {
+    // 16 bytes of source -> 8 (u16) or 16 (u8) LDS samples
+    constexpr int CH = 16 / sizeof(ST);
+    if (vec && col + CH <= sw) {
+        if constexpr (sizeof(ST) == 2) {
+            *reinterpret_cast<uint4 *>(lds_dst) = *reinterpret_cast<const uint4 *>(g + col);
+        } else {
+            const uint4 v = *reinterpret_cast<const uint4 *>(g + col);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            uint4 lo, hi;
+            // widen 16 bytes to 16 u16 (byte permutes, no per-byte shifts)
+            lo.x = __builtin_amdgcn_perm(0, w[0], 0x0c010c00u);
+            lo.y = __builtin_amdgcn_perm(0, w[0], 0x0c030c02u);
+            lo.z = __builtin_amdgcn_perm(0, w[1], 0x0c010c00u);
+            lo.w = __builtin_amdgcn_perm(0, w[1], 0x0c030c02u);
+            hi.x = __builtin_amdgcn_perm(0, w[2], 0x0c010c00u);
+            hi.y = __builtin_amdgcn_perm(0, w[2], 0x0c030c02u);
+            hi.z = __builtin_amdgcn_perm(0, w[3], 0x0c010c00u);
+            hi.w = __builtin_amdgcn_perm(0, w[3], 0x0c030c02u);
+            reinterpret_cast<uint4 *>(lds_dst)[0] = lo;
+            reinterpret_cast<uint4 *>(lds_dst)[1] = hi;
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < CH; ++e) lds_dst[e] = (col + e < sw) ? static_cast<uint16_t>(g[col + e]) : 0;
+    }
+}
+
+template <typename ST, int OUTB, int HT>
+__global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
+    extern __shared__ __align__(16) uint16_t lds[];
+    const int frame = blockIdx.y;
+    int t = blockIdx.x;
+    int p = 0;
+    if (a.nplanes > 1 && t >= a.pl[1].tile_base) p = 1;
+    if (a.nplanes > 2 && t >= a.pl[2].tile_base) p = 2;
+    const PlaneJob &J = a.pl[p];
+    t -= J.tile_base;
+    const int ty = t / J.tiles_x, tx = t - ty * J.tiles_x;
+    const int x0 = tx * kTileW, nx = min(kTileW, J.dw - x0);
+    const int y0 = ty * J.th, ny = min(J.th, J.dh - y0);
+    const int c0 = J.tile_c0[tx], cn = J.tile_cn[tx];
+    const int r0 = J.tile_r0[ty], rn = J.tile_rn[ty];
+    const int S = J.S;
+    uint16_t *src_t = lds;                                           // [R][S]
+    int16_t *inter = reinterpret_cast<int16_t *>(lds + J.R * S);     // [R][256]
+    const int tid = threadIdx.x;
+
+    // ---- stage the source window in LDS -----------------------------------
+    {
+        constexpr int CH = 16 / sizeof(ST);
+        const ST *base = reinterpret_cast<const ST *>(a.src[p] + frame * a.sfs[p]);
+        const int cpr = (cn + CH - 1) / CH;
+        const int total = rn * cpr;
+        for (int id = tid; id < total; id += kThreads) {
+            const int r = id / cpr, ch = id - r * cpr;
+            const ST *g = reinterpret_cast<const ST *>(reinterpret_cast<const uint8_t *>(base) +
+                                                       (int64_t)(r0 + r) * a.sls[p]);
+            stage_chunk<ST>(src_t + r * S + ch * CH, g, c0 + ch * CH, J.sw, a.vec_src);
+        }
+    }
+    __syncthreads();
+
+    // ---- horizontal pass: one output column per lane, all staged rows -------
+    if (tid < nx) {
+        const int x = x0 + tid;
+        const int off = J.hpos[x] - c0;
+        int c[HT];
+#pragma unroll
+        for (int k = 0; k < HT; ++k) c[k] = J.hcoef[(int64_t)x * HT + k];
+        const uint16_t *s = src_t + off;
+        for (int r = 0; r < rn; ++r) {
+            int acc = 0;
+#pragma unroll
+            for (int k = 0; k < HT; ++k) acc += static_cast<int>(s[k]) * c[k];
+            acc >>= a.hshift;
+            inter[r * kTileW + tid] = static_cast<int16_t>(acc < 32767 ? acc : 32767);
+            s += S;
+        }
+    }
+    __syncthreads();
+
+    // ---- vertical pass: wave-uniform row, 4 adjacent outputs per lane ------
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int cx = lane * 4;
+    uint8_t *dbase = a.dst[p] + frame * a.dfs[p];
+    const int vt = J.vt;
+    for (int yy = wave; yy < ny; yy += kThreads / 64) {
+        const int y = y0 + yy;
+        const int lr = J.vpos[y] - r0;
+        const int16_t *vc = J.vcoef + (int64_t)y * vt;
+        int acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
+        if (cx < nx) {
+            const int16_t *row = inter + lr * kTileW + cx;
+            for (int k = 0; k < vt; ++k) {
+                const int cf = vc[k];
+                const uint2 q = *reinterpret_cast<const uint2 *>(row + k * kTileW);
+                acc0 += static_cast<int>(static_cast<int16_t>(q.x & 0xffff)) * cf;
+                acc1 += static_cast<int>(static_cast<int16_t>(q.x >> 16)) * cf;
+                acc2 += static_cast<int>(static_cast<int16_t>(q.y & 0xffff)) * cf;
+                acc3 += static_cast<int>(static_cast<int16_t>(q.y >> 16)) * cf;
+            }
+            const int x = x0 + cx;
+            int o[4];
+            if constexpr (OUTB == 8) {
+                const int drow = y & 7;
+                int d[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) d[j] = a.dither ? c_dither[drow][(x + j + J.dither_off) & 7] : 64;
+                o[0] = (acc0 + (d[0] << 12)) >> 19;
+                o[1] = (acc1 + (d[1] << 12)) >> 19;
+                o[2] = (acc2 + (d[2] << 12)) >> 19;
+                o[3] = (acc3 + (d[3] << 12)) >> 19;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[j] = min(max(o[j], 0), 255);
+                uint8_t *drow_p = dbase + (int64_t)y * a.dls[p];
+                if (a.vec_dst && x + 3 < J.dw) {
+                    *reinterpret_cast<uint32_t *>(drow_p + x) =
+                        (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | ((uint32_t)o[3] << 24);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (x + j < J.dw) drow_p[x + j] = (uint8_t)o[j];
+                }
+            } else {
+                constexpr int sh = 11 + 16 - OUTB;
+                constexpr int mx = (1 << OUTB) - 1;
+                o[0] = (acc0 + (1 << (sh - 1))) >> sh;
+                o[1] = (acc1 + (1 << (sh - 1))) >> sh;
+                o[2] = (acc2 + (1 << (sh - 1))) >> sh;
+                o[3] = (acc3 + (1 << (sh - 1))) >> sh;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[j] = min(max(o[j], 0), mx);
+                uint16_t *drow_p = reinterpret_cast<uint16_t *>(dbase + (int64_t)y * a.dls[p]);
+                if (a.vec_dst && x + 3 < J.dw) {
+                    uint2 v;
+                    v.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+                    v.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+                    *reinterpret_cast<uint2 *>(drow_p + x) = v;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (x + j < J.dw) drow_p[x + j] = (uint16_t)o[j];
+                }
+            }
+        }
+    }
+}
+
+// planarCopyWrapper (same subsampling, same or wider depth): 8 samples per lane.
+__global__ __launch_bounds__(256) void copy_widen_kernel(const uint8_t *src, int64_t sls, int64_t sfs, int sbytes,
+                                                         uint8_t *dst, int64_t dls, int64_t dfs, int dbytes,
+                                                         int w, int h, int shift) {
+    const int frame = blockIdx.z;
+    const int y = blockIdx.y;
+    const uint8_t *s = src + frame * sfs + (int64_t)y * sls;
+    uint8_t *d = dst + frame * dfs + (int64_t)y * dls;
+    for (int x = (blockIdx.x * 256 + threadIdx.x) * 8; x < w; x += gridDim.x * 256 * 8) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            if (x + e >= w) break;
+            const int v = sbytes == 1 ? s[x + e] : reinterpret_cast<const uint16_t *>(s)[x + e];
+            if (dbytes == 1)
+                d[x + e] = (uint8_t)v;
+            else
+                reinterpret_cast<uint16_t *>(d)[x + e] = (uint16_t)(v << shift);
+        }
+    }
+}
+
+// yuv422pToUyvyWrapper: interleave U Y V Y (8-bit); one lane writes 16 bytes.
+__global__ __launch_bounds__(256) void interleave_uyvy_kernel(const uint8_t *Y, const uint8_t *U, const uint8_t *V,
+                                                              int64_t yls, int64_t uls, int64_t vls, int64_t yfs,
+                                                              int64_t ufs, int64_t vfs, uint8_t *dst, int64_t dls,
+                                                              int64_t dfs, int w, int h) {
+    const int frame = blockIdx.z, y = blockIdx.y;
+    const uint8_t *yr = Y + frame * yfs + (int64_t)y * yls;
+    const uint8_t *ur = U + frame * ufs + (int64_t)y * uls;
+    const uint8_t *vr = V + frame * vfs + (int64_t)y * vls;
+    uint8_t *d = dst + frame * dfs + (int64_t)y * dls;
+    const int pairs = (w + 1) / 2;
+    for (int q = (blockIdx.x * 256 + threadIdx.x) * 4; q < pairs; q += gridDim.x * 256 * 4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int i = q + e;
+            if (i >= pairs) break;
+            d[4 * i + 0] = ur[i];
+            d[4 * i + 1] = yr[2 * i];
+            d[4 * i + 2] = vr[i];
+            d[4 * i + 3] = (2 * i + 1 < w) ? yr[2 * i + 1] : 0;
+        }
+    }
+}
+
+using KernelFn = void (*)(const ScaleArgs);
+
+template <typename ST, int OUTB>
+KernelFn pick_ht(int ht) {
+    switch (ht) {
+    case 1: return scale_kernel<ST, OUTB, 1>;
+    case 2: return scale_kernel<ST, OUTB, 2>;
+    case 4: return scale_kernel<ST, OUTB, 4>;
+    case 6: return scale_kernel<ST, OUTB, 6>;
+    case 8: return scale_kernel<ST, OUTB, 8>;
+    case 12: return scale_kernel<ST, OUTB, 12>;
+    case 16: return scale_kernel<ST, OUTB, 16>;
+    case 24: return scale_kernel<ST, OUTB, 24>;
+    case 32: return scale_kernel<ST, OUTB, 32>;
+    default: return nullptr;
+    }
+}
+
+inline int ht_bucket(int t) {
+    static const int b[] = {1, 2, 4, 6, 8, 12, 16, 24, 32};
+    for (int v : b)
+        if (t <= v) return v;
+    return -1;
+}
+
+} // namespace pp
+
+// ---------------------------------------------------------------------------
+struct pp_scale_plan {
+    enum Kind { GENERIC, COPY, INTERLEAVE, GENERIC_UYVY } kind = GENERIC;
+    pp_ctx *ctx = nullptr;
+    int src_fmt = 0, dst_fmt = 0, sw = 0, sh = 0, dw = 0, dh = 0;
+    pp::FmtInfo si{}, di{};
+    int csw = 0, csh = 0, cdw = 0, cdh = 0;
+    pp::FilterBank f[4];   // hl, hc, vl, vc (FFmpeg layout)
+    int ht = 1;            // compiled H-tap bucket
+    pp::PlaneJob job[3]{};
+    void *dev = nullptr;   // all tables in one allocation
+    void *scratch = nullptr; int64_t scratch_plane[3] = {0, 0, 0}; // GENERIC_UYVY planar 4:2:2 temp
+    int scratch_frames = 0;
+    size_t lds_bytes = 0;
+};
+
+namespace {
+
+using pp::FilterBank;
+
+struct HostPlane {
+    FilterBank::Compact h, v;
+    std::vector<int32_t> c0, cn, r0, rn;
+    int tiles_x = 0, tiles_y = 0, th = 0, R = 0, S = 0;
+};
+
+// Choose the tile height and the staged windows for one plane.
+int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::string *err) {
+    static const int ths[] = {32, 16, 8, 4, 2, 1};
+    hp.tiles_x = (dw + pp::kTileW - 1) / pp::kTileW;
+    hp.c0.assign(hp.tiles_x, 0);
+    hp.cn.assign(hp.tiles_x, 0);
+    int S = 0;
+    for (int tx = 0; tx < hp.tiles_x; ++tx) {
+        int lo = sw, hi = 0;
+        for (int x = tx * pp::kTileW; x < std::min(dw, (tx + 1) * pp::kTileW); ++x) {
+            lo = std::min(lo, hp.h.pos[x]);
+            hi = std::max(hi, hp.h.pos[x] + hp.h.taps);
+        }
+        lo &= ~15;
+        int n = (hi - lo + 15) & ~15;
+        hp.c0[tx] = lo;
+        hp.cn[tx] = n;
+        S = std::max(S, n);
+    }
+    for (int th : ths) {
+        const int ty_n = (dh + th - 1) / th;
+        int R = 0;
+        std::vector<int32_t> r0(ty_n), rn(ty_n);
+        for (int ty = 0; ty < ty_n; ++ty) {
+            int lo = sh, hi = 0;
+            for (int y = ty * th; y < std::min(dh, (ty + 1) * th); ++y) {
+                lo = std::min(lo, hp.v.pos[y]);
+                hi = std::max(hi, hp.v.pos[y] + hp.v.taps);
+            }
+            r0[ty] = lo;
+            rn[ty] = hi - lo;
+            R = std::max(R, hi - lo);
+        }
+        const size_t bytes = (size_t)R * S * 2 + (size_t)R * pp::kTileW * 2;
+        if (bytes <= (size_t)pp::kLdsBudget || th == 1) {
+            if (bytes > 64 * 1024) {
+                *err = "scale ratio too large for one LDS tile";
+                return -1;
+            }
+            hp.th = th; hp.tiles_y = ty_n; hp.R = R; hp.S = S;
+            hp.r0 = r0; hp.rn = rn;
+            *lds = std::max(*lds, bytes);
+            return 0;
+        }
+    }
+    return -1;
+}
+
+}  // namespace
+
+extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, int dw, int dh,
+                                    int flags, double p0, double p1, pp_scale_plan **out) {
+    using namespace pp;
+    if (!out) PP_FAIL(PP_ERR_INVALID, "null argument");
+    *out = nullptr;  // ctx == NULL: host-only plan (tables for introspection, no device upload)
+    FmtInfo si = fmt_info(src_fmt), di = fmt_info(dst_fmt);
+    if (!si.valid || si.packed) PP_FAIL(PP_ERR_INVALID, "source format %d must be planar YUV", src_fmt);
+    if (!di.valid || dst_fmt == PP_FMT_V210) PP_FAIL(PP_ERR_INVALID, "destination format %d unsupported", dst_fmt);
+    if (sw < 4 || sh < 4 || dw < 1 || dh < 1 || sw > 16384 || sh > 16384 || dw > 16384 || dh > 16384)
+        PP_FAIL(PP_ERR_INVALID, "bad dimensions %dx%d -> %dx%d", sw, sh, dw, dh);
+    if (!(flags & (PP_SWS_BICUBIC | PP_SWS_LANCZOS | PP_SWS_BILINEAR)))
+        PP_FAIL(PP_ERR_UNSUPPORTED, "flags 0x%x: only bicubic, lanczos, bilinear", flags);
+
+    std::unique_ptr<pp_scale_plan> P(new pp_scale_plan());
+    P->ctx = ctx;
+    P->src_fmt = src_fmt; P->dst_fmt = dst_fmt;
+    P->sw = sw; P->sh = sh; P->dw = dw; P->dh = dh;
+    P->si = si; P->di = di;
+    P->csw = ceil_rshift(sw, si.hsub); P->csh = ceil_rshift(sh, si.vsub);
+    P->cdw = ceil_rshift(dw, di.hsub); P->cdh = ceil_rshift(dh, di.vsub);
+
+    // ff_get_unscaled_swscale(): converters tried before the generic path.
+    if (sw == dw && sh == dh) {
+        if (src_fmt == PP_FMT_YUV422P && dst_fmt == PP_FMT_UYVY422) {
+            P->kind = pp_scale_plan::INTERLEAVE;
+            *out = P.release();
+            return PP_OK;
+        }
+        if (!di.packed && si.hsub == di.hsub && si.vsub == di.vsub && si.depth <= di.depth) {
+            P->kind = pp_scale_plan::COPY;
+            *out = P.release();
+            return PP_OK;
+        }
+    }
+    P->kind = di.packed ? pp_scale_plan::GENERIC_UYVY : pp_scale_plan::GENERIC;
+
+    // sws_init_context(): increments and siting (get_local_pos, default -513)
+    std::string err;
+    const int lumXInc = (int)((((int64_t)sw << 16) + (dw >> 1)) / dw);
+    const int lumYInc = (int)((((int64_t)sh << 16) + (dh >> 1)) / dh);
+    const int chrXInc = (int)((((int64_t)P->csw << 16) + (P->cdw >> 1)) / P->cdw);
+    const int chrYInc = (int)((((int64_t)P->csh << 16) + (P->cdh >> 1)) / P->cdh);
+    if (P->f[0].build(lumXInc, sw, dw, 4, 1 << 14, flags, p0, p1, local_pos(0), local_pos(0), &err) ||
+        P->f[1].build(chrXInc, P->csw, P->cdw, 4, 1 << 14, flags, p0, p1, local_pos(si.hsub), local_pos(di.hsub), &err) ||
+        P->f[2].build(lumYInc, sh, dh, 2, 1 << 12, flags, p0, p1, local_pos(0), local_pos(0), &err) ||
+        P->f[3].build(chrYInc, P->csh, P->cdh, 2, 1 << 12, flags, p0, p1, local_pos(si.vsub), local_pos(di.vsub), &err))
+        PP_FAIL(PP_ERR_UNSUPPORTED, "filter construction: %s", err.c_str());
+
+    // GPU layout: compact windows, one H-tap bucket for the launch
+    HostPlane hp[2];
+    for (int c = 0; c < 2; ++c) {
+        const int src_w = c ? P->csw : sw, src_h = c ? P->csh : sh;
+        if (P->f[c].compact(src_w, 1, &hp[c].h, &err) || P->f[2 + c].compact(src_h, 1, &hp[c].v, &err))
+            PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
+    }
+    const int ht = ht_bucket(std::max(hp[0].h.taps, hp[1].h.taps));
+    if (ht < 0) PP_FAIL(PP_ERR_UNSUPPORTED, "horizontal filter of %d taps", std::max(hp[0].h.taps, hp[1].h.taps));
+    P->ht = ht;
+    for (int c = 0; c < 2; ++c) {
+        const int src_w = c ? P->csw : sw, src_h = c ? P->csh : sh;
+        const int dst_w = c ? P->cdw : dw, dst_h = c ? P->cdh : dh;
+        if (hp[c].h.taps != ht && P->f[c].compact(src_w, ht, &hp[c].h, &err))
+            PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
+        if (plan_tiles(hp[c], src_w, src_h, dst_w, dst_h, &P->lds_bytes, &err))
+            PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
+    }
+
+    if (!ctx) {
+        *out = P.release();
+        return PP_OK;
+    }
+    // one device allocation for every table
+    auto sz4 = [](size_t n) { return (n * 4 + 255) & ~size_t(255); };
+    auto sz2 = [](size_t n) { return (n * 2 + 255) & ~size_t(255); };
+    size_t total = 0;
+    for (int c = 0; c < 2; ++c)
+        total += sz4(hp[c].h.pos.size()) + sz2(hp[c].h.coef.size()) + sz4(hp[c].v.pos.size()) +
+                 sz2(hp[c].v.coef.size()) + 2 * sz4(hp[c].c0.size()) + 2 * sz4(hp[c].r0.size());
+    PP_HIP(hipSetDevice(ctx->device));
+    PP_HIP(hipMalloc(&P->dev, total));
+    std::vector<uint8_t> host(total, 0);
+    size_t off = 0;
+    const int32_t *dptr32[2][6];
+    const int16_t *dptr16[2][2];
+    auto put = [&](const void *src, size_t bytes, size_t padded) {
+        std::memcpy(host.data() + off, src, bytes);
+        const void *d = static_cast<uint8_t *>(P->dev) + off;
+        off += padded;
+        return d;
+    };
+    for (int c = 0; c < 2; ++c) {
+        dptr32[c][0] = (const int32_t *)put(hp[c].h.pos.data(), hp[c].h.pos.size() * 4, sz4(hp[c].h.pos.size()));
+        dptr16[c][0] = (const int16_t *)put(hp[c].h.coef.data(), hp[c].h.coef.size() * 2, sz2(hp[c].h.coef.size()));
+        dptr32[c][1] = (const int32_t *)put(hp[c].v.pos.data(), hp[c].v.pos.size() * 4, sz4(hp[c].v.pos.size()));
+        dptr16[c][1] = (const int16_t *)put(hp[c].v.coef.data(), hp[c].v.coef.size() * 2, sz2(hp[c].v.coef.size()));
+        dptr32[c][2] = (const int32_t *)put(hp[c].c0.data(), hp[c].c0.size() * 4, sz4(hp[c].c0.size()));
+        dptr32[c][3] = (const int32_t *)put(hp[c].cn.data(), hp[c].cn.size() * 4, sz4(hp[c].cn.size()));
+        dptr32[c][4] = (const int32_t *)put(hp[c].r0.data(), hp[c].r0.size() * 4, sz4(hp[c].r0.size()));
+        dptr32[c][5] = (const int32_t *)put(hp[c].rn.data(), hp[c].rn.size() * 4, sz4(hp[c].rn.size()));
+    }
+    PP_HIP(hipMemcpy(P->dev, host.data(), total, hipMemcpyHostToDevice));
+
+    int base = 0;
+    for (int p = 0; p < 3; ++p) {
+        const int c = p ? 1 : 0;
+        PlaneJob &J = P->job[p];
+        J.sw = c ? P->csw : sw; J.sh = c ? P->csh : sh;
+        J.dw = c ? P->cdw : dw; J.dh = c ? P->cdh : dh;
+        J.tiles_x = hp[c].tiles_x; J.tiles_y = hp[c].tiles_y; J.th = hp[c].th;
+        J.tile_base = base;
+        base += J.tiles_x * J.tiles_y;
+        J.vt = hp[c].v.taps; J.R = hp[c].R; J.S = hp[c].S;
+        J.dither_off = p == 2 ? 3 : 0;
+        J.hpos = dptr32[c][0]; J.hcoef = dptr16[c][0];
+        J.vpos = dptr32[c][1]; J.vcoef = dptr16[c][1];
+        J.tile_c0 = dptr32[c][2]; J.tile_cn = dptr32[c][3];
+        J.tile_r0 = dptr32[c][4]; J.tile_rn = dptr32[c][5];
+    }
+    *out = P.release();
+    return PP_OK;
+}
+
+extern "C" int pp_scale_plan_destroy(pp_scale_plan *P) {
+    if (!P) return PP_OK;
+    if (P->dev) (void)hipFree(P->dev);
+    if (P->scratch) (void)hipFree(P->scratch);
+    delete P;
+    return PP_OK;
+}
+
+extern "C" int pp_scale_plan_filter(const pp_scale_plan *P, int which, int16_t *coef, int32_t *pos, int capacity) {
+    if (!P || which < 0 || which > 3) PP_FAIL(PP_ERR_INVALID, "bad plan/which");
+    if (P->kind == pp_scale_plan::COPY || P->kind == pp_scale_plan::INTERLEAVE) return 0;
+    const pp::FilterBank &f = P->f[which];
+    if ((int64_t)f.n * f.size > capacity) PP_FAIL(PP_ERR_INVALID, "capacity %d < %d", capacity, f.n * f.size);
+    std::memcpy(coef, f.coef.data(), f.coef.size() * 2);
+    std::memcpy(pos, f.pos.data(), f.pos.size() * 4);
+    return f.size;
+}
+
+namespace {
+
+bool aligned(const void *p, int64_t ls, int64_t fs, int a) {
+    return ((uintptr_t)p % a) == 0 && ls % a == 0 && fs % a == 0;
+}
+
+int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, int nframes, hipStream_t st,
+                   int out_depth, bool allow_dither) {
+    using namespace pp;
+    ScaleArgs a{};
+    a.nplanes = 3;
+    for (int p = 0; p < 3; ++p) {
+        a.pl[p] = P->job[p];
+        a.src[p] = static_cast<const uint8_t *>(src->data[p]);
+        a.sls[p] = src->linesize[p];
+        a.sfs[p] = src->frame_stride[p];
+        a.dst[p] = static_cast<uint8_t *>(dst->data[p]);
+        a.dls[p] = dst->linesize[p];
+        a.dfs[p] = dst->frame_stride[p];
+    }
+    a.hshift = P->si.depth == 8 ? 7 : P->si.depth - 1;
+    a.dither = allow_dither && P->si.depth > 8 && out_depth == 8;
+    a.vec_src = 1;
+    a.vec_dst = 1;
+    for (int p = 0; p < 3; ++p) {
+        a.vec_src &= aligned(a.src[p], a.sls[p], nframes > 1 ? a.sfs[p] : 0, 16);
+        a.vec_dst &= aligned(a.dst[p], a.dls[p], nframes > 1 ? a.dfs[p] : 0, out_depth == 8 ? 4 : 8);
+    }
+    KernelFn k;
+    if (P->si.depth == 8)
+        k = out_depth == 8 ? pick_ht<uint8_t, 8>(P->ht) : pick_ht<uint8_t, 10>(P->ht);
+    else
+        k = out_depth == 8 ? pick_ht<uint16_t, 8>(P->ht) : pick_ht<uint16_t, 10>(P->ht);
+    if (!k) PP_FAIL(PP_ERR_UNSUPPORTED, "no kernel for %d taps", P->ht);
+    const int tiles = P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y;
+    for (int f0 = 0; f0 < nframes; f0 += 65535) {
+        const int nf = std::min(65535, nframes - f0);
+        ScaleArgs b = a;
+        for (int p = 0; p < 3; ++p) {
+            b.src[p] += f0 * a.sfs[p];
+            b.dst[p] += f0 * a.dfs[p];
+        }
+        hipLaunchKernelGGL(k, dim3(tiles, nf), dim3(kThreads), P->lds_bytes, st, b);
+    }
+    PP_HIP(hipGetLastError());
+    return PP_OK;
+}
+
+}  // namespace
+
+extern "C" int pp_scale_execute(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, int nframes,
+                                void *stream) {
+    using namespace pp;
+    if (!P || !src || !dst || nframes < 0) PP_FAIL(PP_ERR_INVALID, "null argument");
+    if (!P->ctx) PP_FAIL(PP_ERR_INVALID, "host-only plan (created without a context) cannot execute");
+    if (nframes == 0) return PP_OK;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    PP_HIP(hipSetDevice(P->ctx->device));
+    const int sbytes = P->si.depth > 8 ? 2 : 1;
+    switch (P->kind) {
+    case pp_scale_plan::COPY: {
+        const int dbytes = P->di.depth > 8 ? 2 : 1;
+        for (int p = 0; p < 3; ++p) {
+            const int w = p ? P->csw : P->sw, h = p ? P->csh : P->sh;
+            dim3 grid((w + 2047) / 2048, h, nframes);
+            hipLaunchKernelGGL(copy_widen_kernel, grid, dim3(256), 0, st, (const uint8_t *)src->data[p],
+                               src->linesize[p], src->frame_stride[p], sbytes, (uint8_t *)dst->data[p],
+                               dst->linesize[p], dst->frame_stride[p], dbytes, w, h, P->di.depth - P->si.depth);
+        }
+        PP_HIP(hipGetLastError());
+        return PP_OK;
+    }
+    case pp_scale_plan::INTERLEAVE: {
+        dim3 grid(((P->sw + 1) / 2 + 1023) / 1024, P->sh, nframes);
+        hipLaunchKernelGGL(interleave_uyvy_kernel, grid, dim3(256), 0, st, (const uint8_t *)src->data[0],
+                           (const uint8_t *)src->data[1], (const uint8_t *)src->data[2], src->linesize[0],
+                           src->linesize[1], src->linesize[2], src->frame_stride[0], src->frame_stride[1],
+                           src->frame_stride[2], (uint8_t *)dst->data[0], dst->linesize[0], dst->frame_stride[0],
+                           P->sw, P->sh);
+        PP_HIP(hipGetLastError());
+        return PP_OK;
+    }
+    case pp_scale_plan::GENERIC:
+        return launch_generic(P, src, dst, nframes, st, P->di.depth, true);
+    case pp_scale_plan::GENERIC_UYVY: {
+        // yuv2packedX: planar 8-bit 4:2:2 (flat rounding) then interleave
+        const int64_t yb = (int64_t)P->dw * P->dh, cb = (int64_t)P->cdw * P->cdh;
+        const int64_t per = yb + 2 * cb;
+        if (P->scratch_frames < nframes) {
+            if (P->scratch) PP_HIP(hipFree(P->scratch));
+            P->scratch = nullptr;
+            PP_HIP(hipMalloc(&P->scratch, per * nframes));
+            P->scratch_frames = nframes;
+        }
+        uint8_t *s = static_cast<uint8_t *>(P->scratch);
+        pp_frames tmp{};
+        tmp.data[0] = s; tmp.data[1] = s + yb * nframes; tmp.data[2] = s + (yb + cb) * nframes;
+        tmp.linesize[0] = P->dw; tmp.linesize[1] = tmp.linesize[2] = P->cdw;
+        tmp.frame_stride[0] = yb; tmp.frame_stride[1] = tmp.frame_stride[2] = cb;
+        // the packed path rounds with 1<<18 and never dithers
+        int rc = launch_generic(P, src, &tmp, nframes, st, 8, false);
+        if (rc) return rc;
+        dim3 grid(((P->dw + 1) / 2 + 1023) / 1024, P->dh, nframes);
+        hipLaunchKernelGGL(interleave_uyvy_kernel, grid, dim3(256), 0, st, (const uint8_t *)tmp.data[0],
+                           (const uint8_t *)tmp.data[1], (const uint8_t *)tmp.data[2], tmp.linesize[0],
+                           tmp.linesize[1], tmp.linesize[2], tmp.frame_stride[0], tmp.frame_stride[1],
+                           tmp.frame_stride[2], (uint8_t *)dst->data[0], dst->linesize[0], dst->frame_stride[0],
+                           P->dw, P->dh);
+        PP_HIP(hipGetLastError());
+        return PP_OK;
+    }
+    }
+    PP_FAIL(PP_ERR_INVALID, "bad plan kind");
+}

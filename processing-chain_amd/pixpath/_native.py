@@ -1,0 +1,82 @@
+"""ctypes binding of libpixpath.so (include/pixpath.h).
+
+The library is the product: there is no CPU fallback.  If it is missing or
+cannot be loaded, every entry point raises immediately (``NativeMissing``).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PIXPATH_LIB", os.path.join(_HERE, "libpixpath.so"))
+
+PP_OK = 0
+ERRORS = {-1: "PP_ERR_INVALID", -2: "PP_ERR_HIP", -3: "PP_ERR_NOMEM", -4: "PP_ERR_UNSUPPORTED"}
+
+# every symbol declared in include/pixpath.h
+EXPORTS = (
+    "pp_abi_version", "pp_last_error", "pp_ctx_create", "pp_ctx_destroy", "pp_plane_bytes",
+    "pp_v210_linesize", "pp_scale_plan_create", "pp_scale_plan_destroy", "pp_scale_plan_filter",
+    "pp_scale_execute", "pp_pad_execute", "pp_v210_pack", "pp_spinner_upload", "pp_stall_compose",
+    "pp_siti", "pp_fps_map",
+)
+
+
+class NativeMissing(RuntimeError):
+    pass
+
+
+class PixpathError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (%d): %s" % (ERRORS.get(code, "?"), code, msg))
+        self.code = code
+
+
+class pp_frames(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p * 3), ("linesize", ctypes.c_int64 * 3),
+                ("frame_stride", ctypes.c_int64 * 3)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libpixpath.so once; raise NativeMissing if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeMissing("libpixpath.so not found at %s -- run `make -C processing-chain_amd` "
+                            "(or __graft_entry__.build())" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
+    fr = ctypes.POINTER(pp_frames)
+    sig = {
+        "pp_abi_version": (i32, []),
+        "pp_last_error": (ctypes.c_char_p, []),
+        "pp_ctx_create": (i32, [i32, ctypes.POINTER(vp)]),
+        "pp_ctx_destroy": (i32, [vp]),
+        "pp_plane_bytes": (i64, [i32, i32, i32, i32, i64]),
+        "pp_v210_linesize": (i64, [i32]),
+        "pp_scale_plan_create": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, dbl, dbl, ctypes.POINTER(vp)]),
+        "pp_scale_plan_destroy": (i32, [vp]),
+        "pp_scale_plan_filter": (i32, [vp, i32, vp, vp, i32]),
+        "pp_scale_execute": (i32, [vp, fr, fr, i32, vp]),
+        "pp_pad_execute": (i32, [vp, i32, i32, i32, fr, i32, i32, i32, i32, fr, i32, vp]),
+        "pp_v210_pack": (i32, [vp, i32, i32, fr, fr, i32, vp]),
+        "pp_spinner_upload": (i32, [vp, i32, vp, i32, i32, i32]),
+        "pp_stall_compose": (i32, [vp, i32, i32, i32, fr, vp, vp, fr, i32, vp]),
+        "pp_siti": (i32, [vp, i32, i32, i32, vp, i64, i64, i32, vp, vp, vp, vp]),
+        "pp_fps_map": (i32, [i32, i64, i64, i64, i64, vp, i32]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc < 0:
+        raise PixpathError(rc, lib().pp_last_error().decode(errors="replace"))
+    return rc

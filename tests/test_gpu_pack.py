@@ -1,0 +1,73 @@
+"""HIP pad / v210 / stall compositing vs the CPU restatement -- bit-exact.
+
+pad: vf_pad (lib/ffmpeg.py:1183, :1209); v210: v210enc (lib/test_config.py:
+208-215); stall: spec PP-STALL-1 (bufferer, p03_generateAvPvs.py:236-243,
+parity unpinned against bufferer itself)."""
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle as po
+import synth
+
+pytestmark = pytest.mark.gpu
+GOLDEN_SPINNER = os.path.join(os.path.dirname(__file__), "golden", "spinner-128-white.png")
+
+
+@pytest.mark.parametrize("fmt,sw,sh,dw,dh", [
+    (po.YUV420P, 1920, 800, 1920, 1080),       # SRC 3840x1600 -> AVPVS 1920x800, PC CPVS
+    (po.YUV422P10LE, 1920, 1012, 1920, 1080),  # 4096x2160 SRC
+    (po.YUV420P10LE, 1280, 533, 1280, 800),    # tablet, odd offset rounded to the chroma grid
+    (po.YUV422P, 31, 17, 64, 40),
+])
+def test_pad_matches_oracle(gpu, fmt, sw, sh, dw, dh):
+    from pixpath import ops
+    from pixpath.frames import FrameBatch
+    rng = np.random.default_rng(3)
+    frames = [synth.noise_frame(rng, fmt, sw, sh) for _ in range(2)]
+    src = FrameBatch.from_numpy(fmt, synth.batch(frames), device=gpu)
+    out = ops.pad(src, dw, dh).to_numpy()
+    for i in range(2):
+        ref = po.pad(fmt, frames[i], dw, dh, (dw - sw) // 2, (dh - sh) // 2)
+        for p in range(3):
+            np.testing.assert_array_equal(out[p][i], ref[p])
+
+
+@pytest.mark.parametrize("w,h", [(1920, 1080), (1280, 720), (100, 7), (52, 3), (8, 2), (10, 2)])
+def test_v210_matches_oracle(gpu, w, h):
+    from pixpath import ops
+    from pixpath.frames import FrameBatch
+    rng = np.random.default_rng(11)
+    # full 10-bit range so the [4, 1019] clip is exercised
+    frames = [[rng.integers(0, 1024, s).astype(np.uint16) for s in po.plane_shapes(po.YUV422P10LE, w, h)]
+              for _ in range(2)]
+    src = FrameBatch.from_numpy(po.YUV422P10LE, synth.batch(frames), device=gpu)
+    out = ops.v210_pack(src).to_numpy()[0]
+    for i in range(2):
+        np.testing.assert_array_equal(out[i], po.v210_pack(frames[i]))
+
+
+@pytest.mark.parametrize("fmt", [po.YUV420P, po.YUV422P10LE, po.YUV420P10LE, po.YUV422P])
+def test_stall_compose_matches_oracle(gpu, fmt):
+    from pixpath import ops, spinner
+    from pixpath.frames import FrameBatch
+    anim, _ = spinner.load_apng(GOLDEN_SPINNER)
+    w, h = 1920, 1080
+    rng = np.random.default_rng(404)
+    frames = [synth.noise_frame(rng, fmt, w, h) for _ in range(3)]
+    src = FrameBatch.from_numpy(fmt, synth.batch(frames), device=gpu)
+    ops.spinner_upload(anim, fmt)
+    src_idx = np.array([2, 2, -1, 0, 1], np.int32)
+    sp_idx = np.array([0, 5, 7, -1, 3], np.int32)
+    out = ops.stall_compose(src, src_idx, sp_idx).to_numpy()
+    depth = po.fmt_info(fmt)[0]
+    for k in range(len(src_idx)):
+        if src_idx[k] >= 0:
+            base = frames[src_idx[k]]
+        else:
+            base = [np.full(s, (16 if p == 0 else 128) << (depth - 8), dtype=po.plane_dtype(fmt))
+                    for p, s in enumerate(po.plane_shapes(fmt, w, h))]
+        ref = base if sp_idx[k] < 0 else po.overlay_spinner(fmt, base, po.spinner_to_yuva(anim[sp_idx[k]], fmt))
+        for p in range(3):
+            np.testing.assert_array_equal(out[p][k], ref[p], err_msg="frame %d plane %d" % (k, p))

@@ -1,0 +1,85 @@
+"""HIP P.910 SI/TI vs the numpy reference (oracle/siti_ref.py) -- 1e-4 relative.
+
+Tolerance (north_star): SI/TI within 1e-4 relative of the numpy reference.
+The kernel's TI moments are exact integers, so TI is compared at 1e-12."""
+import numpy as np
+import pytest
+
+import siti_ref
+import synth
+import pyoracle as po
+
+pytestmark = pytest.mark.gpu
+RTOL_SI = 1e-4
+
+
+def _run(frames, depth, gpu, prev=None):
+    import torch
+    from pixpath import ops
+    dt = torch.uint16 if depth > 8 else torch.uint8
+    t = torch.from_numpy(np.ascontiguousarray(frames.astype(np.uint16 if depth > 8 else np.uint8))).to(gpu)
+    pt = None
+    if prev is not None:
+        pt = torch.from_numpy(np.ascontiguousarray(prev.astype(np.uint16 if depth > 8 else np.uint8))).to(gpu)
+    assert t.dtype == dt
+    si, ti = ops.siti(t, depth, prev=pt)
+    torch.cuda.synchronize()
+    return si.cpu().numpy(), ti.cpu().numpy()
+
+
+@pytest.mark.parametrize("depth,w,h,content", [
+    (8, 1920, 1080, "smooth"), (10, 1920, 1080, "smooth"), (8, 1920, 1080, "noise"),
+    (10, 3840, 2160, "smooth"), (8, 333, 97, "noise"), (10, 2050, 33, "noise"), (8, 3, 3, "noise"),
+])
+def test_siti_matches_numpy(gpu, depth, w, h, content):
+    fmt = po.YUV420P10LE if depth > 8 else po.YUV420P
+    rng = np.random.default_rng(910)
+    n = 4
+    if content == "smooth":
+        frames = np.stack([synth.smooth_frame(t, fmt, w, h)[0] for t in range(n)])
+    else:
+        frames = np.stack([synth.noise_frame(rng, fmt, w, h)[0] for _ in range(n)])
+    si, ti = _run(frames, depth, gpu)
+    rsi, rti = siti_ref.siti(frames)
+    np.testing.assert_allclose(si, rsi, rtol=RTOL_SI, atol=1e-9)
+    assert np.isnan(ti[0]) and np.isnan(rti[0])
+    np.testing.assert_allclose(ti[1:], rti[1:], rtol=1e-12, atol=1e-12)
+
+
+def test_siti_known_answers(gpu):
+    # constant frames: SI = TI = 0; a static repeated frame: TI = 0
+    c = np.full((3, 64, 80), 100, np.uint8)
+    si, ti = _run(c, 8, gpu)
+    assert np.all(si == 0) and np.all(ti[1:] == 0)
+    # vertical edge: step of 100 at column 40 -> Sobel |Gx| = 400 on two columns
+    e = np.zeros((2, 32, 80), np.uint8)
+    e[:, :, 40:] = 100
+    si, _ = _run(e, 8, gpu)
+    rsi, _ = siti_ref.siti(e)
+    np.testing.assert_allclose(si, rsi, rtol=1e-12)
+    # global brightness step of +5 between frames: TI = 0 (std of a constant)
+    g = np.stack([np.full((16, 16), 50, np.uint8), np.full((16, 16), 55, np.uint8)])
+    _, ti = _run(g, 8, gpu)
+    assert ti[1] == 0
+
+
+def test_siti_prev_halo_equals_single_pass(gpu):
+    """Frame-range sharding with a 1-frame halo reproduces the single pass."""
+    frames = np.stack([synth.smooth_frame(t, po.YUV420P10LE, 640, 360)[0] for t in range(9)])
+    si, ti = _run(frames, 10, gpu)
+    si_a, ti_a = _run(frames[:4], 10, gpu)
+    si_b, ti_b = _run(frames[4:], 10, gpu, prev=frames[3])
+    np.testing.assert_array_equal(np.concatenate([si_a, si_b]), si)
+    np.testing.assert_array_equal(np.concatenate([ti_a, ti_b])[1:], ti[1:])
+
+
+def test_siti_config2_length(gpu):
+    """600 frames (config 2 length) against the C oracle on every 50th frame."""
+    frames = np.stack([synth.smooth_frame(t % 37, po.YUV420P10LE, 1920, 1080)[0] for t in range(600)])
+    si, ti = _run(frames, 10, gpu)
+    idx = np.arange(1, 600, 50)
+    for i in idx:
+        rsi = siti_ref.si_frame(frames[i])
+        rti = siti_ref.ti_frame(frames[i], frames[i - 1])
+        assert abs(si[i] - rsi) <= RTOL_SI * abs(rsi)
+        assert abs(ti[i] - rti) <= 1e-12 * max(1.0, abs(rti))
