@@ -9,16 +9,18 @@
 // dither = ff_dither_8x8_128[row & 7][(col + off) & 7] when a >8-bit source is
 // narrowed to 8 bit (off = 3 for the V plane), flat 64 otherwise.
 //
-// MI355X design: one workgroup (256 lanes = 4 wave64) owns a 256-wide x TH-tall
-// output tile of one plane of one frame.  It stages the source window
-// (R rows x S cols, 16-B vector loads) in LDS, runs the horizontal pass
-// LDS->LDS (15-bit int16 intermediates, coefficients in VGPRs, one output
-// column per lane), then the vertical pass LDS->HBM with wave-uniform
-// coefficients (scalar loads) and 4 outputs per lane (ds_read_b64 of 4
-// intermediates per tap).  Intermediates never touch HBM: traffic is one read
-// of the source (+ L2-served halo rows) and one write of the output.
-// All three planes of a whole frame batch go in ONE launch
-// (blockIdx.x = tile over the planes, blockIdx.y = frame).
+// MI355X design ("strip streaming"): one workgroup (256 lanes = 4 wave64) owns
+// a TW-wide (256 unless a large downscale needs narrower) column strip of one
+// plane of one frame, split vertically into a few segments, and walks it top to
+// bottom in chunks of CHO output rows.  Per chunk it stages only the source
+// rows not seen before (16-B vector loads -> LDS), runs the horizontal pass
+// LDS->LDS into a ring of 15-bit intermediate rows (coefficients in VGPRs, one
+// output column per lane), then the vertical pass ring->HBM with wave-uniform
+// coefficients (scalar loads) and 4 outputs per lane (one ds_read_b64 per tap).
+// Every source row is read from HBM once per strip (plus a few rows at segment
+// seams and a column halo of ~taps/TW), intermediates never touch HBM, and all
+// three planes of a whole frame batch go in ONE launch
+// (blockIdx.x = strip x segment over the planes, blockIdx.y = frame).
 #include <algorithm>
 #include <cstring>
 #include <memory>
@@ -28,7 +30,7 @@
 
 namespace pp {
 
-constexpr int kTileW = 256;      // output columns per workgroup
+constexpr int kTileW = 256;      // widest output tile (columns); narrower for large downscales
 constexpr int kThreads = 256;    // 4 waves
 constexpr int kLdsBudget = 40 * 1024;
 
@@ -41,15 +43,16 @@ __constant__ uint8_t c_dither[8][8] = {
 
 struct PlaneJob {
     int sw, sh, dw, dh;
-    int tiles_x, tiles_y, tile_base, th;
-    int vt, R, S;         // V taps, staged rows / cols (max over tiles)
+    int tiles_x, tiles_y, tile_base;  // strips x vertical segments, first block index
+    int tw, seg_h, cho;   // strip width, output rows per segment, output rows per chunk
+    int vt, ring, maxnew, S; // V taps, ring rows (pow2), staged rows per chunk, staged cols
     int dither_off;       // 0 (Y, U) or 3 (V)
     const int32_t *hpos;  // [dw]   window start (absolute source column)
     const int16_t *hcoef; // [dw * HT]
     const int32_t *vpos;  // [dh]
     const int16_t *vcoef; // [dh * vt]
-    const int32_t *tile_c0, *tile_cn; // [tiles_x] staged column window
-    const int32_t *tile_r0, *tile_rn; // [tiles_y] staged row window
+    const int32_t *tile_c0, *tile_cn; // [tiles_x] staged column window per strip
+    const int32_t *chunk_lo, *chunk_hi; // [ceil(dh/cho)] source rows needed by each chunk
 };
 
 struct ScaleArgs {
@@ -104,66 +107,81 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     if (a.nplanes > 2 && t >= a.pl[2].tile_base) p = 2;
     const PlaneJob &J = a.pl[p];
     t -= J.tile_base;
-    const int ty = t / J.tiles_x, tx = t - ty * J.tiles_x;
-    const int x0 = tx * kTileW, nx = min(kTileW, J.dw - x0);
-    const int y0 = ty * J.th, ny = min(J.th, J.dh - y0);
+    const int seg = t / J.tiles_x, tx = t - seg * J.tiles_x;
+    const int TW = J.tw;
+    const int x0 = tx * TW, nx = min(TW, J.dw - x0);
     const int c0 = J.tile_c0[tx], cn = J.tile_cn[tx];
-    const int r0 = J.tile_r0[ty], rn = J.tile_rn[ty];
-    const int S = J.S;
-    uint16_t *src_t = lds;                                           // [R][S]
-    int16_t *inter = reinterpret_cast<int16_t *>(lds + J.R * S);     // [R][256]
+    const int S = J.S, mask = J.ring - 1;
+    uint16_t *src_t = lds;                                              // [maxnew][S]
+    int16_t *ring = reinterpret_cast<int16_t *>(lds + J.maxnew * S);    // [ring][TW]
     const int tid = threadIdx.x;
-
-    // ---- stage the source window in LDS -----------------------------------
-    {
-        constexpr int CH = 16 / sizeof(ST);
-        const ST *base = reinterpret_cast<const ST *>(a.src[p] + frame * a.sfs[p]);
-        const int cpr = (cn + CH - 1) / CH;
-        const int total = rn * cpr;
-        for (int id = tid; id < total; id += kThreads) {
-            const int r = id / cpr, ch = id - r * cpr;
-            const ST *g = reinterpret_cast<const ST *>(reinterpret_cast<const uint8_t *>(base) +
-                                                       (int64_t)(r0 + r) * a.sls[p]);
-            stage_chunk<ST>(src_t + r * S + ch * CH, g, c0 + ch * CH, J.sw, a.vec_src);
-        }
-    }
-    __syncthreads();
-
-    // ---- horizontal pass: one output column per lane, all staged rows -------
-    if (tid < nx) {
-        const int x = x0 + tid;
-        const int off = J.hpos[x] - c0;
-        int c[HT];
-#pragma unroll
-        for (int k = 0; k < HT; ++k) c[k] = J.hcoef[(int64_t)x * HT + k];
-        const uint16_t *s = src_t + off;
-        for (int r = 0; r < rn; ++r) {
-            int acc = 0;
-#pragma unroll
-            for (int k = 0; k < HT; ++k) acc += static_cast<int>(s[k]) * c[k];
-            acc >>= a.hshift;
-            inter[r * kTileW + tid] = static_cast<int16_t>(acc < 32767 ? acc : 32767);
-            s += S;
-        }
-    }
-    __syncthreads();
-
-    // ---- vertical pass: wave-uniform row, 4 adjacent outputs per lane ------
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int lane = tid & 63;
-    const int cx = lane * 4;
+    const ST *sbase = reinterpret_cast<const ST *>(a.src[p] + frame * a.sfs[p]);
     uint8_t *dbase = a.dst[p] + frame * a.dfs[p];
+
+    // horizontal-pass lane mapping: one output column per lane, r_step rows at a time
+    const int col = tid % TW, r_first = tid / TW, r_step = kThreads / TW;
+    int hc[HT];
+    int hoff = 0;
+    if (col < nx) {
+        const int x = x0 + col;
+        hoff = J.hpos[x] - c0;
+#pragma unroll
+        for (int k = 0; k < HT; ++k) hc[k] = J.hcoef[(int64_t)x * HT + k];
+    }
+    // vertical-pass lane mapping: 4 adjacent outputs per lane
+    const int groups = TW / 4;
+    const int lane_g = tid % groups, row_first = tid / groups, row_step = kThreads / groups;
+    const int cx = lane_g * 4;
     const int vt = J.vt;
-    for (int yy = wave; yy < ny; yy += kThreads / 64) {
-        const int y = y0 + yy;
-        const int lr = J.vpos[y] - r0;
-        const int16_t *vc = J.vcoef + (int64_t)y * vt;
-        int acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
-        if (cx < nx) {
-            const int16_t *row = inter + lr * kTileW + cx;
+
+    const int y_begin = seg * J.seg_h, y_end = min(J.dh, y_begin + J.seg_h);
+    int next_src = J.chunk_lo[y_begin / J.cho];
+    for (int y0 = y_begin; y0 < y_end; y0 += J.cho) {
+        const int ci = y0 / J.cho;
+        const int lo = J.chunk_lo[ci], hi = J.chunk_hi[ci];
+        if (next_src < lo) next_src = lo;
+        const int nnew = hi - next_src;
+        // ---- stage the new source rows [next_src, hi) -----------------------
+        if (nnew > 0) {
+            constexpr int CH = 16 / sizeof(ST);
+            const int cpr = (cn + CH - 1) / CH;
+            const int total = nnew * cpr;
+            for (int id = tid; id < total; id += kThreads) {
+                const int r = id / cpr, ch = id - r * cpr;
+                const ST *g = reinterpret_cast<const ST *>(reinterpret_cast<const uint8_t *>(sbase) +
+                                                           (int64_t)(next_src + r) * a.sls[p]);
+                stage_chunk<ST>(src_t + r * S + ch * CH, g, c0 + ch * CH, J.sw, a.vec_src);
+            }
+        }
+        __syncthreads();  // staged rows visible; the previous chunk's vertical pass is done
+        // ---- horizontal pass into the ring --------------------------------------
+        if (nnew > 0 && col < nx) {
+            const uint16_t *s = src_t + r_first * S + hoff;
+            for (int r = r_first; r < nnew; r += r_step) {
+                int acc = 0;
+#pragma unroll
+                for (int k = 0; k < HT; ++k) acc += static_cast<int>(s[k]) * hc[k];
+                acc >>= a.hshift;
+                ring[((next_src + r) & mask) * TW + col] = static_cast<int16_t>(acc < 32767 ? acc : 32767);
+                s += r_step * S;
+            }
+        }
+        if (nnew > 0) next_src = hi;
+        __syncthreads();
+        // ---- vertical pass: output rows [y0, y0 + cho) --------------------------
+        const int ny = min(J.cho, y_end - y0);
+        for (int yy0 = row_first; yy0 < ny + row_first; yy0 += row_step) {
+            int yy = yy0;
+            if (TW == kTileW) yy = __builtin_amdgcn_readfirstlane(yy);
+            if (yy >= ny) break;
+            const int y = y0 + yy;
+            const int vp = J.vpos[y];
+            const int16_t *vc = J.vcoef + (int64_t)y * vt;
+            if (cx >= nx) continue;
+            int acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
             for (int k = 0; k < vt; ++k) {
                 const int cf = vc[k];
-                const uint2 q = *reinterpret_cast<const uint2 *>(row + k * kTileW);
+                const uint2 q = *reinterpret_cast<const uint2 *>(ring + ((vp + k) & mask) * TW + cx);
                 acc0 += static_cast<int>(static_cast<int16_t>(q.x & 0xffff)) * cf;
                 acc1 += static_cast<int>(static_cast<int16_t>(q.x >> 16)) * cf;
                 acc2 += static_cast<int>(static_cast<int16_t>(q.y & 0xffff)) * cf;
@@ -310,55 +328,89 @@ using pp::FilterBank;
 
 struct HostPlane {
     FilterBank::Compact h, v;
-    std::vector<int32_t> c0, cn, r0, rn;
-    int tiles_x = 0, tiles_y = 0, th = 0, R = 0, S = 0;
+    std::vector<int32_t> c0, cn, lo, hi;
+    int tiles_x = 0, nseg = 0, tw = 0, seg_h = 0, cho = 0, ring = 0, maxnew = 0, S = 0;
 };
 
-// Choose the tile height and the staged windows for one plane.
-int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::string *err) {
-    static const int ths[] = {32, 16, 8, 4, 2, 1};
-    hp.tiles_x = (dw + pp::kTileW - 1) / pp::kTileW;
-    hp.c0.assign(hp.tiles_x, 0);
-    hp.cn.assign(hp.tiles_x, 0);
+// Column window of every strip for a strip width.
+int col_windows(HostPlane &hp, int sw, int dw, int tw) {
+    const int tiles_x = (dw + tw - 1) / tw;
+    hp.c0.assign(tiles_x, 0);
+    hp.cn.assign(tiles_x, 0);
     int S = 0;
-    for (int tx = 0; tx < hp.tiles_x; ++tx) {
+    for (int tx = 0; tx < tiles_x; ++tx) {
         int lo = sw, hi = 0;
-        for (int x = tx * pp::kTileW; x < std::min(dw, (tx + 1) * pp::kTileW); ++x) {
+        for (int x = tx * tw; x < std::min(dw, (tx + 1) * tw); ++x) {
             lo = std::min(lo, hp.h.pos[x]);
             hi = std::max(hi, hp.h.pos[x] + hp.h.taps);
         }
         lo &= ~15;
-        int n = (hi - lo + 15) & ~15;
+        const int n = (hi - lo + 15) & ~15;
         hp.c0[tx] = lo;
         hp.cn[tx] = n;
         S = std::max(S, n);
     }
-    for (int th : ths) {
-        const int ty_n = (dh + th - 1) / th;
-        int R = 0;
-        std::vector<int32_t> r0(ty_n), rn(ty_n);
-        for (int ty = 0; ty < ty_n; ++ty) {
-            int lo = sh, hi = 0;
-            for (int y = ty * th; y < std::min(dh, (ty + 1) * th); ++y) {
-                lo = std::min(lo, hp.v.pos[y]);
-                hi = std::max(hi, hp.v.pos[y] + hp.v.taps);
-            }
-            r0[ty] = lo;
-            rn[ty] = hi - lo;
-            R = std::max(R, hi - lo);
+    return S;
+}
+
+// Row windows per chunk of `cho` output rows; returns (max new rows per chunk, ring rows).
+void row_chunks(HostPlane &hp, int sh, int dh, int cho, int seg_h, int *maxnew, int *ring) {
+    const int nch = (dh + cho - 1) / cho;
+    hp.lo.assign(nch, 0);
+    hp.hi.assign(nch, 0);
+    int span = 1;
+    for (int ci = 0; ci < nch; ++ci) {
+        int lo = sh, hi = 0;
+        for (int y = ci * cho; y < std::min(dh, (ci + 1) * cho); ++y) {
+            lo = std::min(lo, hp.v.pos[y]);
+            hi = std::max(hi, hp.v.pos[y] + hp.v.taps);
         }
-        const size_t bytes = (size_t)R * S * 2 + (size_t)R * pp::kTileW * 2;
-        if (bytes <= (size_t)pp::kLdsBudget || th == 1) {
-            if (bytes > 64 * 1024) {
-                *err = "scale ratio too large for one LDS tile";
-                return -1;
-            }
-            hp.th = th; hp.tiles_y = ty_n; hp.R = R; hp.S = S;
-            hp.r0 = r0; hp.rn = rn;
+        hp.lo[ci] = lo;
+        hp.hi[ci] = hi;
+        span = std::max(span, hi - lo);
+    }
+    // simulate the kernel's walk to size the staging buffer
+    int mn = 0;
+    for (int y0 = 0; y0 < dh; y0 += seg_h) {
+        int next = hp.lo[y0 / cho];
+        for (int y = y0; y < std::min(dh, y0 + seg_h); y += cho) {
+            const int ci = y / cho;
+            if (next < hp.lo[ci]) next = hp.lo[ci];
+            mn = std::max(mn, hp.hi[ci] - next);
+            next = std::max(next, hp.hi[ci]);
+        }
+    }
+    int r = 1;
+    while (r < span) r <<= 1;
+    *maxnew = std::max(mn, 1);
+    *ring = r;
+}
+
+// Strip width / chunk height / segments for one plane: the widest strip and
+// tallest chunk whose LDS (staging + ring) fits the budget; ~256-row segments.
+int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::string *err) {
+    static const int tws[] = {256, 128, 64, 32};
+    static const int chos[] = {32, 16, 8, 4, 2, 1};
+    for (int tw : tws) {
+        if (tw > 32 && tw / 2 >= dw) continue;  // narrower strips suffice for this plane
+        const int S = col_windows(hp, sw, dw, tw);
+        for (int cho : chos) {
+            int nseg = std::max(1, (dh + 128) / 256);
+            int seg_h = (dh + nseg - 1) / nseg;
+            seg_h = (seg_h + cho - 1) / cho * cho;
+            nseg = (dh + seg_h - 1) / seg_h;
+            int maxnew, ring;
+            row_chunks(hp, sh, dh, cho, seg_h, &maxnew, &ring);
+            const size_t bytes = (size_t)maxnew * S * 2 + (size_t)ring * tw * 2;
+            if (bytes > (size_t)pp::kLdsBudget) continue;
+            hp.tiles_x = (dw + tw - 1) / tw;
+            hp.nseg = nseg; hp.tw = tw; hp.seg_h = seg_h; hp.cho = cho;
+            hp.ring = ring; hp.maxnew = maxnew; hp.S = S;
             *lds = std::max(*lds, bytes);
             return 0;
         }
     }
+    *err = "scale ratio too large for the LDS budget";
     return -1;
 }
 
@@ -441,7 +493,7 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
     size_t total = 0;
     for (int c = 0; c < 2; ++c)
         total += sz4(hp[c].h.pos.size()) + sz2(hp[c].h.coef.size()) + sz4(hp[c].v.pos.size()) +
-                 sz2(hp[c].v.coef.size()) + 2 * sz4(hp[c].c0.size()) + 2 * sz4(hp[c].r0.size());
+                 sz2(hp[c].v.coef.size()) + 2 * sz4(hp[c].c0.size()) + 2 * sz4(hp[c].lo.size());
     PP_HIP(hipSetDevice(ctx->device));
     PP_HIP(hipMalloc(&P->dev, total));
     std::vector<uint8_t> host(total, 0);
@@ -461,8 +513,8 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
         dptr16[c][1] = (const int16_t *)put(hp[c].v.coef.data(), hp[c].v.coef.size() * 2, sz2(hp[c].v.coef.size()));
         dptr32[c][2] = (const int32_t *)put(hp[c].c0.data(), hp[c].c0.size() * 4, sz4(hp[c].c0.size()));
         dptr32[c][3] = (const int32_t *)put(hp[c].cn.data(), hp[c].cn.size() * 4, sz4(hp[c].cn.size()));
-        dptr32[c][4] = (const int32_t *)put(hp[c].r0.data(), hp[c].r0.size() * 4, sz4(hp[c].r0.size()));
-        dptr32[c][5] = (const int32_t *)put(hp[c].rn.data(), hp[c].rn.size() * 4, sz4(hp[c].rn.size()));
+        dptr32[c][4] = (const int32_t *)put(hp[c].lo.data(), hp[c].lo.size() * 4, sz4(hp[c].lo.size()));
+        dptr32[c][5] = (const int32_t *)put(hp[c].hi.data(), hp[c].hi.size() * 4, sz4(hp[c].hi.size()));
     }
     PP_HIP(hipMemcpy(P->dev, host.data(), total, hipMemcpyHostToDevice));
 
@@ -472,15 +524,16 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
         PlaneJob &J = P->job[p];
         J.sw = c ? P->csw : sw; J.sh = c ? P->csh : sh;
         J.dw = c ? P->cdw : dw; J.dh = c ? P->cdh : dh;
-        J.tiles_x = hp[c].tiles_x; J.tiles_y = hp[c].tiles_y; J.th = hp[c].th;
+        J.tiles_x = hp[c].tiles_x; J.tiles_y = hp[c].nseg; J.tw = hp[c].tw;
+        J.seg_h = hp[c].seg_h; J.cho = hp[c].cho;
         J.tile_base = base;
         base += J.tiles_x * J.tiles_y;
-        J.vt = hp[c].v.taps; J.R = hp[c].R; J.S = hp[c].S;
+        J.vt = hp[c].v.taps; J.ring = hp[c].ring; J.maxnew = hp[c].maxnew; J.S = hp[c].S;
         J.dither_off = p == 2 ? 3 : 0;
         J.hpos = dptr32[c][0]; J.hcoef = dptr16[c][0];
         J.vpos = dptr32[c][1]; J.vcoef = dptr16[c][1];
         J.tile_c0 = dptr32[c][2]; J.tile_cn = dptr32[c][3];
-        J.tile_r0 = dptr32[c][4]; J.tile_rn = dptr32[c][5];
+        J.chunk_lo = dptr32[c][4]; J.chunk_hi = dptr32[c][5];
     }
     *out = P.release();
     return PP_OK;

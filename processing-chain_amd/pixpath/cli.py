@@ -1,0 +1,365 @@
+"""`python -m pixpath.cli` -- the GPU-backend commands that pixpath.ffmpeg's
+builders return (same positional output file, -y/-n overwrite convention as
+the ffmpeg strings they replace).
+
+  avpvs  decode -> scale (+ -pix_fmt conversion) [-> fps] [-> long-test canvas] -> encode
+         (create_avpvs_short lib/ffmpeg.py:940, create_avpvs_segment :1003)
+  cpvs   decode AVPVS -> fps -> [pad] -> uyvy422 / v210 packing -> encode
+         (create_cpvs PC branch lib/ffmpeg.py:1177-1201)
+  stall  AVPVS -> stall frames (frozen/black + spinner) or frame freezing
+         (bufferer call p03_generateAvPvs.py:236-243, spec PP-STALL-1)
+  siti   P.910 SI/TI of a SRC (util/SRC_analysis.py hook)
+
+Inputs/outputs ending in .y4m or .raw/.yuv are read/written directly;
+anything else goes through ffmpeg pipes.  The device is chosen by
+PIXPATH_DEVICE, else by process id modulo the visible GPU count (one process
+per GPU under the reference's ParallelRunner).
+"""
+import argparse
+import ast
+import json
+import os
+import sys
+from fractions import Fraction
+
+import numpy as np
+
+
+def _device():
+    import torch
+    n = torch.cuda.device_count()
+    if n == 0:
+        raise SystemExit("pixpath: no GPU visible")
+    d = os.environ.get("PIXPATH_DEVICE")
+    return int(d) if d is not None else os.getpid() % n
+
+
+class CountingWriter:
+    """Writer wrapper: caps the frame count (-t), remembers the last frame (canvas repeat)."""
+
+    def __init__(self, inner, frame_bytes, cap=None):
+        self.inner, self.fb, self.cap, self.n, self.last = inner, frame_bytes, cap, 0, None
+
+    def write(self, frames):
+        mv = memoryview(frames).cast("B")
+        k = len(mv) // self.fb
+        if self.cap is not None:
+            k = min(k, self.cap - self.n)
+        if k <= 0:
+            return
+        self.inner.write(mv[:k * self.fb])
+        self.last = bytes(mv[(k - 1) * self.fb:k * self.fb])
+        self.n += k
+
+    def close(self):
+        self.inner.close()
+
+
+def _open_writer(path, fmt, w, h, rate, vopts, aopts, audio_from, overwrite):
+    from . import formats, io as pio
+    ext = os.path.splitext(path)[1].lower()
+    if ext == ".y4m":
+        return pio.Y4MWriter(path, fmt, w, h, rate)
+    if ext in (".raw", ".yuv"):
+        return pio.RawWriter(path)
+    return pio.FFmpegWriter(path, fmt, w, h, rate, vopts, aopts, audio_from=audio_from,
+                            overwrite="-y" if overwrite else "-n")  # pragma: no cover
+
+
+def _skip(path, overwrite):
+    if not overwrite and os.path.isfile(path):
+        print("pixpath: output %s exists, not overwriting (-y to force)" % path, file=sys.stderr)
+        return True
+    return False
+
+
+def _fps_counts(in_rate, out_rate):
+    """emit(k): how many output frames show input frame k under vf_fps rounding=near."""
+    a, b = Fraction(in_rate), Fraction(out_rate)
+    N, D = a.denominator * b.numerator, a.numerator * b.denominator
+
+    def t(i):
+        return (2 * i * N + D) // (2 * D)
+    return lambda k: t(k + 1) - t(k)
+
+
+def cmd_avpvs(args):
+    import torch
+    from . import formats, io as pio, ops
+    from .pipeline import Pipeline, Stage
+    out = args.output
+    if _skip(out, args.y):
+        return 0
+    dev = _device()
+    torch.cuda.set_device(dev)
+    rd = pio.open_reader(args.input)
+    W, H = (int(v) for v in args.size.split("x"))
+    target = formats.fmt(args.pix_fmt)
+    rate = Fraction(args.fps) if args.fps else rd.rate
+    if args.overlay_yuv420:
+        # create_avpvs_segment: scale into the overlay's yuv420p, then -pix_fmt conversion
+        s1 = ops.Scaler(rd.fmt, rd.w, rd.h, "yuv420p", W, H, flags=args.flags)
+        s2 = None if target.name == "yuv420p" else ops.Scaler("yuv420p", W, H, target, W, H, flags="bicubic")
+        mid = {}
+
+        def process(src, dst, stream):
+            if s2 is None:
+                s1(src, dst, stream=stream)
+                return
+            n = src.n
+            m = mid.get(n)
+            if m is None:
+                from .frames import FrameBatch
+                m = mid[n] = FrameBatch("yuv420p", W, H, n, device=src.device)
+            s1(src, m, stream=stream)
+            s2(m, dst, stream=stream)
+        stage = Stage(rd.fmt, rd.w, rd.h, target, W, H, process)
+    else:
+        sc = ops.Scaler(rd.fmt, rd.w, rd.h, target, W, H, flags=args.flags)
+        stage = Stage(rd.fmt, rd.w, rd.h, target, W, H, lambda s, d, st: sc(s, d, stream=st))
+    fb = formats.frame_bytes(target, W, H)
+    cap = int(round(float(args.duration) * float(rate))) if args.duration else None
+    inner = _open_writer(out, target, W, H, rate, args.vopts, args.aopts,
+                         None if args.aopts.strip() == "-an" else args.input, args.y)
+    wr = CountingWriter(inner, fb, cap)
+    emit = _fps_counts(rd.rate, rate) if args.fps else None
+    Pipeline(stage, batch=args.batch, device=dev).run(rd, wr, emit=emit)
+    if cap is not None and wr.last is not None:
+        while wr.n < cap:  # overlay eof_action=repeat: the canvas keeps the last frame
+            wr.write(wr.last)
+    rd.close()
+    wr.close()
+    return 0
+
+
+def cmd_cpvs(args):
+    import torch
+    from . import formats, io as pio, ops
+    from .frames import FrameBatch
+    from .pipeline import Pipeline, Stage
+    out = args.output
+    if _skip(out, args.y):
+        return 0
+    dev = _device()
+    torch.cuda.set_device(dev)
+    rd = pio.open_reader(args.input)
+    W, H = (rd.w, rd.h) if not args.pad else (int(v) for v in args.pad.split("x"))
+    W, H = int(W), int(H)
+    cur_fmt = rd.fmt
+    steps = []
+    if args.pad:
+        steps.append(("pad", W, H))
+    if args.vcodec == "rawvideo" and args.pix_fmt == "uyvy422":
+        out_fmt = formats.fmt("uyvy422")
+        steps.append(("scale", ops.Scaler(cur_fmt, W, H, "uyvy422", W, H, flags="bicubic")))
+    elif args.vcodec == "v210":
+        out_fmt = formats.fmt("v210")
+        if cur_fmt.name != "yuv422p10le":
+            steps.append(("scale", ops.Scaler(cur_fmt, W, H, "yuv422p10le", W, H, flags="bicubic")))
+        steps.append(("v210",))
+    else:  # -a/--rawvideo: keep the AVPVS format
+        out_fmt = cur_fmt
+    cache = {}
+
+    def tmp(key, f, n, dev_):
+        t = cache.get((key, n))
+        if t is None:
+            t = cache[(key, n)] = FrameBatch(f, W, H, n, device=dev_)
+        return t
+
+    def process(src, dst, stream):
+        cur = src
+        for i, st in enumerate(steps):
+            last = i == len(steps) - 1
+            if st[0] == "pad":
+                nxt = dst if last else tmp("pad", cur.fmt, cur.n, cur.device)
+                ops.pad(cur, W, H, dst=nxt, stream=stream)
+            elif st[0] == "scale":
+                nxt = dst if last else tmp("scale", st[1].dst_fmt, cur.n, cur.device)
+                st[1](cur, nxt, stream=stream)
+            else:
+                nxt = dst
+                ops.v210_pack(cur, dst=nxt, stream=stream)
+            cur = nxt
+        if not steps:
+            for p in range(len(dst.planes)):
+                dst.view(p).copy_(src.view(p))
+    stage = Stage(rd.fmt, rd.w, rd.h, out_fmt, W, H, process)
+    inner = _open_writer(out, out_fmt, W, H, Fraction(args.fps), "-c:v %s" % args.vcodec + (
+        "" if args.vcodec == "v210" else " -pix_fmt %s" % args.pix_fmt), args.aopts, args.input, args.y)
+    emit = _fps_counts(rd.rate, Fraction(args.fps))
+    Pipeline(stage, batch=args.batch, device=dev).run(rd, inner, emit=emit)
+    rd.close()
+    inner.close()
+    return 0
+
+
+def stall_schedule(buffer_events, rate, n_in, skipping, spinner_delays=None, black_frame=True):
+    """PP-STALL-1 output sequence for an AVPVS of n_in frames at `rate`.
+
+    Returns a list of (src_index, spinner_index): src_index -1 = black frame,
+    spinner_index -1 = no overlay.  Stalls ([media_t, dur]) insert round(dur*rate)
+    frames after frame round(media_t*rate)-1 showing that frame (black when the
+    stall is at t=0 and black_frame is set) with the spinner animated at its own
+    frame delays; freezes ([t, dur], skipping) replace the frames of [t, t+dur)
+    by the frame before t, keeping the length."""
+    rate = Fraction(rate)
+    seq = [(i, -1) for i in range(n_in)]
+    if skipping:
+        for t, d in sorted(buffer_events):
+            a = int(round(t * rate))
+            b = min(n_in, int(round((t + d) * rate)))
+            for i in range(a, b):
+                seq[i] = (max(a - 1, 0), -1)
+        return seq
+    delays = list(spinner_delays) if spinner_delays is not None else [0.0]
+    period = sum(delays)
+    out, cursor = [], 0
+    for t, d in sorted(buffer_events):
+        at = min(n_in, int(round(t * rate)))
+        out.extend(seq[cursor:at])
+        cursor = at
+        frozen = at - 1 if at > 0 else (-1 if black_frame else 0)
+        k = int(round(d * rate))
+        for j in range(k):
+            ts = (j / float(rate)) % period if period > 0 else 0.0
+            acc, si = 0.0, 0
+            for si, dl in enumerate(delays):
+                acc += dl
+                if ts < acc:
+                    break
+            out.append((frozen, si))
+    out.extend(seq[cursor:])
+    return out
+
+
+def cmd_stall(args):
+    import torch
+    from . import formats, io as pio, ops, spinner
+    from .frames import FrameBatch
+    out = args.output
+    if _skip(out, args.y):
+        return 0
+    dev = _device()
+    torch.cuda.set_device(dev)
+    rd = pio.open_reader(args.input)
+    fmt = rd.fmt
+    events = ast.literal_eval(args.buffer)
+    fb = rd.frame_bytes
+    # the AVPVS is decoded once into host memory (the stall schedule indexes it)
+    frames = []
+    while True:
+        buf = np.empty((64, fb), np.uint8)
+        k = rd.read_into(buf, 64)
+        if k:
+            frames.append(buf[:k])
+        if k < 64:
+            break
+    allf = np.concatenate(frames) if frames else np.empty((0, fb), np.uint8)
+    n_in = allf.shape[0]
+    delays = None
+    if not args.skipping:
+        anim, delays = spinner.load_apng(args.spinner)
+        ops.spinner_upload(anim, fmt, device=dev)
+    seq = stall_schedule(events, rd.rate, n_in, args.skipping, delays, black_frame=args.black_frame)
+    wr = _open_writer(out, fmt, rd.w, rd.h, rd.rate, args.vopts, args.aopts, None, args.y)
+    # frames without overlay pass through untouched; stall frames are composed on the GPU in batches
+    i = 0
+    while i < len(seq):
+        s, sp = seq[i]
+        if sp < 0:
+            wr.write(allf[s] if s >= 0 else _black(fmt, rd.w, rd.h))
+            i += 1
+            continue
+        j = i
+        while j < len(seq) and seq[j][1] >= 0 and j - i < 256:
+            j += 1
+        block = seq[i:j]
+        srcs = sorted({b[0] for b in block if b[0] >= 0})
+        remap = {s_: k for k, s_ in enumerate(srcs)}
+        src_b = FrameBatch.interleaved(fmt, rd.w, rd.h, max(1, len(srcs)), device=torch.device("cuda", dev))
+        if srcs:
+            src_b.storage.copy_(torch.from_numpy(allf[srcs]).to(src_b.storage.device))
+        dst_b = FrameBatch.interleaved(fmt, rd.w, rd.h, len(block), device=torch.device("cuda", dev))
+        ops.stall_compose(src_b, [remap.get(b[0], -1) if b[0] >= 0 else -1 for b in block],
+                          [b[1] for b in block], dst=dst_b)
+        wr.write(dst_b.storage.cpu().numpy())
+        i = j
+    rd.close()
+    wr.close()
+    return 0
+
+
+def _black(fmt, w, h):
+    from . import formats, io as pio
+    planes = [np.full((1, r, c), (16 if p == 0 else 128) << (fmt.depth - 8),
+                      np.uint16 if fmt.bytes_per_sample == 2 else np.uint8)
+              for p, (r, c) in enumerate(formats.plane_shapes(fmt, w, h))]
+    return pio.join_planes(planes)
+
+
+def cmd_siti(args):
+    from . import siti
+    si, ti = siti.siti_of_file(args.input, batch=args.batch)
+    SI, TI = siti.siti_summary(si, ti)
+    res = {"file": os.path.basename(args.input), "si": SI, "ti": TI, "frames": int(len(si))}
+    if args.per_frame:
+        res["si_frames"] = [float(v) for v in si]
+        res["ti_frames"] = [None if np.isnan(v) else float(v) for v in ti]
+    print(json.dumps(res))
+    return 0
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="pixpath.cli")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+
+    def common(p):
+        g = p.add_mutually_exclusive_group()
+        g.add_argument("-y", action="store_true", help="overwrite output")
+        g.add_argument("-n", action="store_true", help="never overwrite (default)")
+        p.add_argument("--input", required=True)
+        p.add_argument("--batch", type=int, default=32)
+        p.add_argument("--vopts", default="-c:v ffv1")
+        p.add_argument("--aopts", default="-an")
+        p.add_argument("output")
+
+    p = sub.add_parser("avpvs")
+    common(p)
+    p.add_argument("--size", required=True)
+    p.add_argument("--flags", default="bicubic")
+    p.add_argument("--pix-fmt", required=True)
+    p.add_argument("--fps", default=None)
+    p.add_argument("--duration", default=None)
+    p.add_argument("--overlay-yuv420", action="store_true")
+    p.set_defaults(fn=cmd_avpvs)
+
+    p = sub.add_parser("cpvs")
+    common(p)
+    p.add_argument("--fps", default="60")
+    p.add_argument("--vcodec", required=True)
+    p.add_argument("--pix-fmt", required=True)
+    p.add_argument("--pad", default=None)
+    p.set_defaults(fn=cmd_cpvs)
+
+    p = sub.add_parser("stall")
+    common(p)
+    p.add_argument("--buffer", required=True)
+    p.add_argument("--pix-fmt", default=None)
+    p.add_argument("--spinner", default=None)
+    p.add_argument("--skipping", action="store_true")
+    p.add_argument("--black-frame", action="store_true")
+    p.set_defaults(fn=cmd_stall)
+
+    p = sub.add_parser("siti")
+    p.add_argument("--input", required=True)
+    p.add_argument("--batch", type=int, default=120)
+    p.add_argument("--per-frame", action="store_true")
+    p.set_defaults(fn=cmd_siti)
+
+    args = ap.parse_args(argv)
+    return args.fn(args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,310 @@
+"""Drop-in for the pixel-path command builders of the reference's lib/ffmpeg.py.
+
+Same function names, signatures, return convention (ONE whitespace-collapsed
+shell string, or None when the output exists and overwrite is False) and error
+convention (logger.error + sys.exit(1)) as the reference.
+
+Two backends, chosen by ``set_backend()`` or the environment variable
+PIXPATH_BACKEND:
+
+* "ffmpeg" (default): the reference's strings, byte-identical (pinned by
+  tests/golden/reference_fixtures.json) -- every pixel op runs inside ffmpeg.
+* "gpu": the pixel work of a builder runs on the MI355X through
+  ``python3 -m pixpath.cli`` (ffmpeg still decodes and encodes; frames cross
+  PCIe once each way and every filter between decode and encode runs as HIP
+  kernels).  Builders without pixel work (stream-copy concat, audio mux,
+  preview) and the x264-encoded mobile/tablet CPVS keep their ffmpeg strings.
+
+Reference functions mirrored (file:line in pnats2avhd/processing-chain):
+  calculate_avpvs_video_dimensions  lib/ffmpeg.py:33
+  create_avpvs_short                lib/ffmpeg.py:940
+  create_avpvs_segment              lib/ffmpeg.py:1003
+  create_avpvs_long_concat          lib/ffmpeg.py:1058
+  simple_encoding                   lib/ffmpeg.py:1108
+  create_cpvs                       lib/ffmpeg.py:1149
+  create_preview                    lib/ffmpeg.py:1250
+  audio_mux                         lib/ffmpeg.py:1262
+  bufferer_command                  p03_generateAvPvs.py:215-243 (inline there)
+"""
+import logging
+import os
+import shlex
+
+from .chain import calculate_avpvs_video_dimensions  # noqa: F401  (re-export, a1)
+from .chain import buffer_string, encode_segment_filter_chain  # noqa: F401
+
+logger = logging.getLogger("main")
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FFV1_OPTS = "-c:v ffv1 -threads 4 -level 3 -coder 1 -context 1 -slicecrc 1"
+
+_backend = os.environ.get("PIXPATH_BACKEND", "ffmpeg")
+
+
+def set_backend(name):
+    global _backend
+    if name not in ("ffmpeg", "gpu"):
+        raise ValueError("backend must be 'ffmpeg' or 'gpu'")
+    _backend = name
+
+
+def get_backend():
+    return _backend
+
+
+def _collapse(cmd):
+    return " ".join(cmd.split())
+
+
+def _skip_existing(output_file, overwrite):
+    """(overwrite_spec, skip): the reference's -y / -n / None convention (lib/ffmpeg.py:964-970)."""
+    if overwrite:
+        return "-y", False
+    if os.path.isfile(output_file):
+        logger.warning("output " + output_file + " already exists, will not convert. Use --force to force overwriting.")
+        return "-n", True
+    return "-n", False
+
+
+def _gpu_cli(sub, args):
+    return "PYTHONPATH={} python3 -m pixpath.cli {} {}".format(shlex.quote(PKG_DIR), sub,
+                                                                " ".join(shlex.quote(str(a)) for a in args))
+
+
+def create_avpvs_short(pvs, overwrite=False, scale_avpvs_tosource=False, force_60_fps=False, post_proc_id=0):
+    """Decode the first segment, upscale to the AVPVS size, FFV1 + FLAC (lib/ffmpeg.py:940-1000)."""
+    test_config = pvs.test_config
+    coding_width = test_config.post_processings[post_proc_id].coding_width
+    coding_height = test_config.post_processings[post_proc_id].coding_height
+    output_file = pvs.get_avpvs_wo_buffer_file_path() if pvs.has_buffering() else pvs.get_avpvs_file_path()
+
+    fps_filter, fps = "", None
+    if scale_avpvs_tosource:
+        fps = pvs.src.get_fps()
+        fps_filter = ",fps={src_framerate}"  # the reference never expands this placeholder
+    elif force_60_fps:
+        fps = 60.0
+        fps_filter = ",fps={src_framerate}"
+
+    overwrite_spec, skip = _skip_existing(output_file, overwrite)
+    if skip:
+        return None
+
+    input_file = pvs.segments[0].get_segment_file_path()
+    target_pix_fmt = pvs.get_pix_fmt_for_avpvs()
+    w, h = calculate_avpvs_video_dimensions(pvs.src.stream_info["coded_width"], pvs.src.stream_info["coded_height"],
+                                            coding_width, coding_height)
+    ql = pvs.segments[0].quality_level
+    if ql.height > h:  # the QL is taller than the AVPVS: use the QL size (lib/ffmpeg.py:981-986)
+        w, h = ql.width, ql.height
+
+    if _backend == "gpu":
+        args = [overwrite_spec, "--input", input_file, "--size", "%dx%d" % (w, h), "--flags", "bicubic",
+                "--pix-fmt", target_pix_fmt, "--vopts", FFV1_OPTS, "--aopts", "-c:a flac"]
+        if fps is not None:  # the GPU path applies the fps the reference intended
+            args += ["--fps", fps]
+        return _collapse(_gpu_cli("avpvs", args + [output_file]))
+
+    cmd = """
+    ffmpeg -nostdin
+    {overwrite_spec}
+    -i {input_file}
+    -filter:v scale={w}:{h}:flags=bicubic{fps_filter},setsar=1/1
+    {FFV1_OPTS}
+    -pix_fmt {target_pix_fmt} -c:a flac
+    {output_file}""".format(FFV1_OPTS=FFV1_OPTS, **locals())
+    return _collapse(cmd)
+
+
+def create_avpvs_segment(seg, pvs, overwrite=False, scale_avpvs_tosource=False):
+    """Long tests: one segment scaled onto a fixed-duration canvas (lib/ffmpeg.py:1003-1055).
+
+    ffmpeg semantics reproduced by the GPU backend: scale to the AVPVS size in
+    the overlay's yuv420p, fps to R, last frame repeated to D*R frames, then the
+    -pix_fmt conversion to the AVPVS format."""
+    test_config = pvs.test_config
+    coding_height = test_config.post_processings[0].coding_height
+    coding_width = test_config.post_processings[0].coding_width
+    w, h = calculate_avpvs_video_dimensions(pvs.src.stream_info["coded_width"], pvs.src.stream_info["coded_height"],
+                                            coding_width, coding_height)
+    target_pix_fmt = pvs.get_pix_fmt_for_avpvs()
+    input_file = seg.get_segment_file_path()
+    output_file = seg.get_tmp_path()
+    overwrite_spec, skip = _skip_existing(output_file, overwrite)
+    if skip:
+        return None
+    src_framerate = pvs.src.get_fps() if scale_avpvs_tosource else 60.0
+    segment_duration = seg.get_segment_duration()
+
+    if _backend == "gpu":
+        args = [overwrite_spec, "--input", input_file, "--size", "%dx%d" % (w, h), "--flags", "bicubic",
+                "--pix-fmt", target_pix_fmt, "--fps", src_framerate, "--duration", segment_duration,
+                "--overlay-yuv420", "--vopts", FFV1_OPTS, "--aopts", "-an"]
+        return _collapse(_gpu_cli("avpvs", args + [output_file]))
+
+    overlay = "-f lavfi -i nullsrc=s={w}x{h}:d={segment_duration}:r={src_framerate}".format(**locals())
+    complex_filter = ("-filter_complex \"[0:v]scale={w}:{h}:flags=bicubic,fps={src_framerate},setsar=1/1[ol_0];"
+                      "[1:v][ol_0]overlay[vout]\"").format(**locals())
+    cmd = """
+    ffmpeg -nostdin
+    {overwrite_spec}
+    -i {input_file}
+    {overlay}
+    {complex_filter}
+    -map "[vout]" -t {segment_duration}
+    {FFV1_OPTS}
+    -pix_fmt {target_pix_fmt}
+    {output_file}
+    """.format(FFV1_OPTS=FFV1_OPTS, **locals())
+    return _collapse(cmd)
+
+
+def create_avpvs_long_concat(pvs, overwrite=False, scale_avpvs_tosource=False):
+    """Stream-copy concat of the decoded segments (lib/ffmpeg.py:1058-1105); writes the
+    concat file list as a side effect, like the reference.  No pixel work: both
+    backends return the same ffmpeg string."""
+    output_file = pvs.get_tmp_wo_audio_path()
+    overwrite_spec, skip = _skip_existing(output_file, overwrite)
+    if skip:
+        return None
+    total = sum([int(s.get_segment_duration()) for s in pvs.segments])
+    tmp_filelist = pvs.get_avpvs_file_list()
+    with open(tmp_filelist, "w+") as fh:
+        for s in pvs.segments:
+            fh.write("file " + s.get_tmp_path() + "\n")
+    cmd = """
+    ffmpeg -nostdin
+    {overwrite_spec}
+    -f concat -safe 0
+    -i {tmp_filelist}
+    -c:v copy -t {total}
+    {output_file}""".format(**locals())
+    return _collapse(cmd)
+
+
+def simple_encoding(pvs, overwrite, input_file, output_file, vopts, aopts="", filters=""):
+    """lib/ffmpeg.py:1108-1146."""
+    overwrite_spec, skip = _skip_existing(output_file, overwrite)
+    if skip:
+        return None
+    cmd = """
+    ffmpeg -nostdin
+    {overwrite_spec}
+    -i {input_file} {filters}
+    {vopts} {aopts}
+    {output_file}""".format(**locals())
+    return _collapse(cmd)
+
+
+def create_cpvs(pvs, post_processing, rawvideo=False, overwrite=False, nonraw_crf=17, mobile_vprofile="high",
+                mobile_preset="fast"):
+    """CPVS for the playback context (lib/ffmpeg.py:1149-1247).  PC/TV: fps, optional
+    letterbox pad, uyvy422 rawvideo or v210 in AVI (GPU backend: fps map + pad +
+    chroma conversion + packing on the MI355X).  Other contexts: x264 (ffmpeg)."""
+    test_config = pvs.test_config
+    input_file = pvs.get_avpvs_file_path()
+    output_file = pvs.get_cpvs_file_path(context=post_processing.processing_type, rawvideo=rawvideo)
+    w, h = calculate_avpvs_video_dimensions(pvs.src.stream_info["coded_width"], pvs.src.stream_info["coded_height"],
+                                            post_processing.coding_width, post_processing.coding_height)
+    aformat_normalize = ""
+    if post_processing.processing_type in ["pc", "tv"]:
+        vcodec, target_pix_fmt = pvs.get_vcodec_and_pix_fmt_for_cpvs(rawvideo=rawvideo)
+        pad = h < post_processing.coding_height
+        if test_config.is_short():
+            pc_aopts = "-an"
+        else:
+            total_duration = str(pvs.hrc.get_long_hrc_duration())
+            pc_aopts = "-ac 2 -c:a pcm_s16le -t {total_duration}".format(**locals())
+        if _backend == "gpu":
+            overwrite_spec, skip = _skip_existing(output_file, overwrite)
+            if skip:
+                return None
+            args = [overwrite_spec, "--input", input_file, "--fps", post_processing.display_frame_rate,
+                    "--vcodec", vcodec, "--pix-fmt", target_pix_fmt, "--aopts", "-af aresample=48000 " + pc_aopts]
+            if pad:
+                args += ["--pad", "%dx%d" % (post_processing.display_width, post_processing.display_height)]
+            cmd = _collapse(_gpu_cli("cpvs", args + [output_file]))
+        else:
+            filters = "-af aresample=48000 -filter:v 'fps=fps={}".format(post_processing.display_frame_rate)
+            if pad:
+                filters += ",pad=width={}:height={}:x=(ow-iw)/2:y=(oh-ih)/2".format(
+                    post_processing.display_width, post_processing.display_height) + "'"
+            else:
+                filters += "'"
+            cmd = simple_encoding(pvs, overwrite, input_file, output_file,
+                                  "-c:v " + vcodec + " -pix_fmt " + target_pix_fmt, pc_aopts, filters)
+    else:
+        mobile_vopts = ("-c:v libx264 -preset {mobile_preset} -pix_fmt yuv420p -crf {nonraw_crf} "
+                        "-profile:v {mobile_vprofile} -movflags faststart").format(**locals())
+        filters = "-filter:v '"
+        if (post_processing.display_height != post_processing.coding_height) or (h < post_processing.coding_height):
+            # the reference's leading comma (lib/ffmpeg.py:1210) is kept verbatim
+            filters += ",pad=width={}:height={}:x=(ow-iw)/2:y=(oh-ih)/2".format(
+                post_processing.display_width, post_processing.display_height) + "'"
+        else:
+            filters += "scale={}:{}:flags=bicubic,setsar=1/1".format(
+                post_processing.display_width, post_processing.display_height) + "'"
+        if test_config.is_short():
+            mobile_aopts = "-an"
+        else:
+            total_duration = str(pvs.hrc.get_long_hrc_duration())
+            aformat_normalize = "-c:a aac -b:a 512k"
+            mobile_aopts = "-c:a aac -b:a 512k -t {total_duration}".format(**locals())
+        cmd = simple_encoding(pvs, overwrite, input_file, output_file, mobile_vopts, mobile_aopts, filters)
+
+    if test_config.is_long():
+        if cmd is None:
+            return
+        cpvs_path = os.path.abspath(test_config.get_cpvs_path())
+        cmd = " ".join([cmd, "&&", "TMP={cpvs_path}".format(**locals()),
+                        "ffmpeg-normalize {output_file} -o {output_file} -f -nt rms {aformat_normalize}".format(
+                            **locals())])
+    return cmd
+
+
+def create_preview(pvs, overwrite=False):
+    """ProRes preview (lib/ffmpeg.py:1250-1259); codec work, ffmpeg in both backends."""
+    return simple_encoding(pvs, overwrite, pvs.get_avpvs_file_path(), pvs.get_preview_file_path(), "-c:v prores",
+                           "-c:a aac")
+
+
+def audio_mux(pvs, overwrite=False):
+    """Mux SRC audio as PCM (lib/ffmpeg.py:1262-1289); no pixel work."""
+    input_file = pvs.get_tmp_wo_audio_path()
+    audio_src = pvs.src.get_src_file_path()
+    output_file = pvs.get_avpvs_wo_buffer_file_path() if pvs.has_buffering() else pvs.get_avpvs_file_path()
+    overwrite_spec, skip = _skip_existing(output_file, overwrite)
+    if skip:
+        return None
+    cmd = """
+    ffmpeg -nostdin
+    {overwrite_spec}
+    -i {input_file}
+    -i {audio_src}
+    -c:v copy -ac 2 -c:a pcm_s16le -map 0:v -map 1:a
+    {output_file}""".format(**locals())
+    return _collapse(cmd)
+
+
+def bufferer_command(pvs, spinner_path, force=False):
+    """The stalling/freezing command p03 builds inline (p03_generateAvPvs.py:223-243).
+
+    ffmpeg backend: the reference's bufferer string.  gpu backend: the PP-STALL-1
+    compositor (frozen frame or black + centred spinner, or frame freezing with
+    skipping) through pixpath.cli."""
+    input_file = pvs.get_avpvs_wo_buffer_file_path()
+    output_file = pvs.get_avpvs_file_path()
+    bufferstring = buffer_string(pvs.get_buff_events_media_time())
+    pix_fmt = pvs.get_pix_fmt_for_avpvs()
+    overwrite_spec = "-f" if force else ""
+    if pvs.has_framefreeze():
+        stalling_type_options = "-e --skipping"
+    else:
+        stalling_type_options = "-s {}".format(spinner_path)
+    if _backend == "gpu":
+        args = ["-y" if force else "-n", "--input", input_file, "--buffer", bufferstring, "--pix-fmt", pix_fmt,
+                "--black-frame", "--vopts", "-c:v ffv1", "--aopts", "-c:a pcm_s16le"]
+        args += ["--skipping"] if pvs.has_framefreeze() else ["--spinner", spinner_path]
+        return _collapse(_gpu_cli("stall", args + [output_file]))
+    return ("bufferer -i {input_file} -o {output_file} -b {bufferstring} --force-framerate --black-frame"
+            " -v ffv1 -a pcm_s16le -x {pix_fmt} {stalling_type_options} {overwrite_spec}").format(**locals())

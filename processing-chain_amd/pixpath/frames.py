@@ -31,6 +31,27 @@ class FrameBatch:
         self.planes = planes
         self.bps = bps
 
+    @classmethod
+    def interleaved(cls, f, w, h, n, device="cuda", storage=None):
+        """Frame-interleaved batch: one [n, frame_bytes] uint8 buffer holding dense
+        Y|U|V frames (the raw pipe / pinned-buffer layout), planes as strided views.
+        One contiguous H2D/D2H copy moves the whole batch."""
+        fm = formats.fmt(f)
+        fb = formats.frame_bytes(fm, w, h)
+        if storage is None:
+            storage = torch.empty((n, fb), dtype=torch.uint8, device=device)
+        flat = storage.reshape(-1)
+        shapes = formats.plane_shapes(fm, w, h)
+        bps = 1 if fm.packed else fm.bytes_per_sample
+        base = flat.view(torch.uint16) if bps == 2 else flat
+        planes, off = [], 0
+        for r, c in shapes:
+            planes.append(base.as_strided((n, r, c), (fb // bps, c, 1), off // bps))
+            off += r * c * bps
+        b = cls(fm, w, h, n, device=device, planes=planes)
+        b.storage = storage
+        return b
+
     @property
     def device(self):
         return self.planes[0].device

@@ -1,0 +1,241 @@
+"""Raw-frame I/O for the host pipeline: Y4M / raw files, and ffmpeg/ffprobe pipes.
+
+ffmpeg stays the bitstream decoder/encoder (as in the reference); between the
+decode pipe and the encode pipe frames are dense raw planes (Y|U|V per frame),
+which is also the layout of the pinned host buffers and of the frame-
+interleaved device batches (pixpath.frames.FrameBatch.interleaved).
+"""
+import json
+import os
+import shlex
+import subprocess
+from fractions import Fraction
+
+import numpy as np
+
+from . import formats
+
+Y4M_TAGS = {
+    "420jpeg": "yuv420p", "420paldv": "yuv420p", "420mpeg2": "yuv420p", "420": "yuv420p",
+    "422": "yuv422p", "444": "yuv444p", "420p10": "yuv420p10le", "422p10": "yuv422p10le", "444p10": "yuv444p10le",
+}
+Y4M_OUT = {"yuv420p": "420mpeg2", "yuv422p": "422", "yuv444p": "444", "yuv420p10le": "420p10",
+           "yuv422p10le": "422p10", "yuv444p10le": "444p10"}
+
+
+class Reader:
+    fmt = None
+    w = h = 0
+    rate = Fraction(60)
+
+    @property
+    def frame_bytes(self):
+        return formats.frame_bytes(self.fmt, self.w, self.h)
+
+    def read_into(self, buf, n):
+        """Fill up to n dense frames into a writable bytes-like `buf`; return frames read."""
+        fb = self.frame_bytes
+        mv = memoryview(buf).cast("B")
+        got = 0
+        while got < n:
+            if not self._read_frame(mv[got * fb:(got + 1) * fb]):
+                break
+            got += 1
+        return got
+
+    def batches(self, n):
+        """Yield lists of [k, rows, cols] numpy planes, k <= n (tests / analysis)."""
+        fb = self.frame_bytes
+        buf = bytearray(fb * n)
+        while True:
+            k = self.read_into(buf, n)
+            if k == 0:
+                return
+            yield split_planes(np.frombuffer(bytes(buf[:k * fb]), np.uint8).reshape(k, fb), self.fmt, self.w, self.h)
+            if k < n:
+                return
+
+    def close(self):
+        pass
+
+
+def split_planes(frames_u8, f, w, h):
+    """[k, frame_bytes] uint8 -> list of [k, rows, cols] planes (views)."""
+    f = formats.fmt(f)
+    out, off = [], 0
+    dt = np.uint16 if f.bytes_per_sample == 2 and not f.packed else np.uint8
+    for r, c in formats.plane_shapes(f, w, h):
+        nb = r * c * (1 if f.packed else f.bytes_per_sample)
+        out.append(frames_u8[:, off:off + nb].view(dt).reshape(-1, r, c))
+        off += nb
+    return out
+
+
+def join_planes(planes):
+    """list of [k, rows, cols] planes -> [k, frame_bytes] uint8."""
+    k = planes[0].shape[0]
+    return np.concatenate([np.ascontiguousarray(p).view(np.uint8).reshape(k, -1) for p in planes], axis=1)
+
+
+def _readexact(fh, mv):
+    n = 0
+    while n < len(mv):
+        k = fh.readinto(mv[n:])
+        if not k:
+            return n
+        n += k
+    return n
+
+
+class Y4MReader(Reader):
+    def __init__(self, path_or_fh):
+        self.fh = open(path_or_fh, "rb") if isinstance(path_or_fh, str) else path_or_fh
+        hdr = self.fh.readline().decode().split()
+        if hdr[0] != "YUV4MPEG2":
+            raise ValueError("not a YUV4MPEG2 stream")
+        tags = {t[0]: t[1:] for t in hdr[1:]}
+        self.w, self.h = int(tags["W"]), int(tags["H"])
+        if "F" in tags:
+            a, b = tags["F"].split(":")
+            self.rate = Fraction(int(a), int(b))
+        self.fmt = formats.fmt(Y4M_TAGS[tags.get("C", "420jpeg")])
+
+    def _read_frame(self, mv):
+        line = self.fh.readline()
+        if not line:
+            return False
+        if not line.startswith(b"FRAME"):
+            raise ValueError("bad Y4M frame header")
+        return _readexact(self.fh, mv) == len(mv)
+
+    def close(self):
+        self.fh.close()
+
+
+class RawReader(Reader):
+    def __init__(self, path_or_fh, f, w, h, rate=60):
+        self.fh = open(path_or_fh, "rb") if isinstance(path_or_fh, str) else path_or_fh
+        self.fmt, self.w, self.h, self.rate = formats.fmt(f), int(w), int(h), Fraction(rate)
+
+    def _read_frame(self, mv):
+        return _readexact(self.fh, mv) == len(mv)
+
+    def close(self):
+        self.fh.close()
+
+
+class FFmpegReader(RawReader):  # pragma: no cover - needs ffmpeg
+    """Decode any container through `ffmpeg ... -f rawvideo -pix_fmt F pipe:1`."""
+
+    def __init__(self, path, f=None, w=None, h=None, rate=None):
+        st = probe(path)["stream"]
+        f = f or st["pix_fmt"]
+        self.proc = subprocess.Popen(["ffmpeg", "-nostdin", "-v", "error", "-i", path, "-f", "rawvideo",
+                                      "-pix_fmt", f, "pipe:1"], stdout=subprocess.PIPE, bufsize=1 << 24)
+        super().__init__(self.proc.stdout, f, w or st["width"], h or st["height"],
+                         rate or Fraction(st["r_frame_rate"]))
+
+    def close(self):
+        self.proc.stdout.close()
+        if self.proc.wait():
+            raise RuntimeError("ffmpeg decode failed")
+
+
+class Writer:
+    def write(self, frames_u8):
+        """frames_u8: [k, frame_bytes] uint8 (or bytes-like of k dense frames)."""
+        raise NotImplementedError
+
+    def close(self):
+        pass
+
+
+class Y4MWriter(Writer):
+    def __init__(self, path, f, w, h, rate=60):
+        self.fh = open(path, "wb")
+        r = Fraction(rate)
+        self.fb = formats.frame_bytes(f, w, h)
+        self.fh.write(("YUV4MPEG2 W%d H%d F%d:%d Ip A1:1 C%s\n" % (w, h, r.numerator, r.denominator,
+                                                                  Y4M_OUT[formats.fmt(f).name])).encode())
+
+    def write(self, frames_u8):
+        mv = memoryview(frames_u8).cast("B")
+        for i in range(len(mv) // self.fb):
+            self.fh.write(b"FRAME\n")
+            self.fh.write(mv[i * self.fb:(i + 1) * self.fb])
+
+    def close(self):
+        self.fh.close()
+
+
+class RawWriter(Writer):
+    def __init__(self, path):
+        self.fh = open(path, "wb")
+
+    def write(self, frames_u8):
+        self.fh.write(memoryview(frames_u8).cast("B"))
+
+    def close(self):
+        self.fh.close()
+
+
+class FFmpegWriter(Writer):  # pragma: no cover - needs ffmpeg
+    """Encode raw frames with the reference's encoder options (e.g. FFV1 / v210 / rawvideo)."""
+
+    def __init__(self, path, f, w, h, rate, vopts, aopts="-an", audio_from=None, overwrite="-y", extra_in=""):
+        r = Fraction(rate)
+        cmd = "ffmpeg -nostdin -v error {ow} -f rawvideo -pix_fmt {pf} -s {w}x{h} -r {num}/{den} -i pipe:0 ".format(
+            ow=overwrite, pf=formats.fmt(f).name if not formats.fmt(f).packed else
+            ("uyvy422" if formats.fmt(f).id == formats.UYVY422 else "yuv422p10le"),
+            w=w, h=h, num=r.numerator, den=r.denominator)
+        if audio_from:
+            cmd += "-i {} -map 0:v -map 1:a? ".format(shlex.quote(audio_from))
+        cmd += "{} {} {} {}".format(extra_in, vopts, aopts, shlex.quote(path))
+        self.proc = subprocess.Popen(cmd, shell=True, stdin=subprocess.PIPE, bufsize=1 << 24)
+
+    def write(self, frames_u8):
+        self.proc.stdin.write(memoryview(frames_u8).cast("B"))
+
+    def close(self):
+        self.proc.stdin.close()
+        if self.proc.wait():
+            raise RuntimeError("ffmpeg encode failed")
+
+
+def open_reader(path, f=None, w=None, h=None, rate=None):
+    ext = os.path.splitext(path)[1].lower()
+    if ext == ".y4m":
+        return Y4MReader(path)
+    if ext in (".raw", ".yuv"):
+        return RawReader(path, f, w, h, rate or 60)
+    return FFmpegReader(path, f, w, h, rate)
+
+
+def probe(path):
+    """ffprobe stream info + packet-size sums (the reference's get_src_info /
+    get_stream_size, lib/ffmpeg.py:566-633, :399-417); Y4M files are parsed."""
+    if path.lower().endswith(".y4m"):
+        r = Y4MReader(path)
+        st = {"width": r.w, "height": r.h, "coded_width": r.w, "coded_height": r.h, "pix_fmt": r.fmt.name,
+              "r_frame_rate": str(r.rate.numerator // r.rate.denominator) if r.rate.denominator == 1 else
+              "%d/%d" % (r.rate.numerator, r.rate.denominator), "codec_name": "rawvideo"}
+        r.close()
+        return {"stream": st, "sizes": {"v": os.path.getsize(path), "a": 0}}
+    out = subprocess.run(["ffprobe", "-loglevel", "error", "-select_streams", "v", "-show_streams", "-of", "json",
+                          path], check=True, capture_output=True).stdout  # pragma: no cover
+    st = json.loads(out)["streams"][0]  # pragma: no cover
+    sizes = {}
+    for sw in ("v", "a"):  # pragma: no cover
+        o = subprocess.run(["ffprobe", "-loglevel", "error", "-select_streams", sw, "-show_entries", "packet=size",
+                            "-of", "compact=p=0:nk=1", path], check=True, capture_output=True).stdout.decode()
+        sizes[sw] = sum(int(x) for x in o.split("\n") if x)
+    return {"stream": st, "sizes": sizes}  # pragma: no cover
+
+
+def segment_info(path):
+    """The subset of get_segment_info (lib/ffmpeg.py:433-563) that get_difficulty reads."""
+    st = probe(path)["stream"]
+    dur = float(st.get("duration", 0.0))
+    return {"file_size": os.path.getsize(path), "video_duration": dur,
+            "video_frame_rate": float(Fraction(st["r_frame_rate"])), "video_width": st["width"],
+            "video_height": st["height"]}

@@ -1,0 +1,139 @@
+"""Host<->device streaming pipeline: pinned double buffers + async copies.
+
+decode pipe --read--> pinned_in[k%2] --H2D (copy stream)--> dev_in[k%2]
+   --kernels (compute stream)--> dev_out[k%2] --D2H (copy stream)--> pinned_out[k%2]
+   --write--> encode pipe
+
+Reading batch k+1 and writing batch k-1 (host threads) overlap the H2D,
+kernels and D2H of batch k; the copy engine and the compute queue are
+separate HIP streams ordered by events, so PCIe traffic overlaps the kernels of
+the neighbouring batch.  Frame layout everywhere is dense Y|U|V per frame.
+"""
+import queue
+import threading
+
+import torch
+
+from . import formats
+from .frames import FrameBatch
+
+
+class Stage:
+    """A 1:1 per-frame transform on device batches: process(src, dst) enqueues kernels."""
+
+    def __init__(self, in_fmt, in_w, in_h, out_fmt, out_w, out_h, process):
+        self.in_fmt, self.in_w, self.in_h = formats.fmt(in_fmt), in_w, in_h
+        self.out_fmt, self.out_w, self.out_h = formats.fmt(out_fmt), out_w, out_h
+        self.process = process
+
+
+class Pipeline:
+    def __init__(self, stage, batch=32, device=None):
+        self.stage = stage
+        self.batch = int(batch)
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        s = stage
+        self.in_fb = formats.frame_bytes(s.in_fmt, s.in_w, s.in_h)
+        self.out_fb = formats.frame_bytes(s.out_fmt, s.out_w, s.out_h)
+        B = self.batch
+        self.h_in = [torch.empty((B, self.in_fb), dtype=torch.uint8).pin_memory() for _ in range(2)]
+        self.h_out = [torch.empty((B, self.out_fb), dtype=torch.uint8).pin_memory() for _ in range(2)]
+        self.d_in = [FrameBatch.interleaved(s.in_fmt, s.in_w, s.in_h, B, device=self.device) for _ in range(2)]
+        self.d_out = [FrameBatch.interleaved(s.out_fmt, s.out_w, s.out_h, B, device=self.device) for _ in range(2)]
+        self.copy_stream = torch.cuda.Stream(self.device)
+        self.compute_stream = torch.cuda.Stream(self.device)
+        self.frames_in = self.frames_out = 0
+
+    def run(self, reader, writer, emit=None):
+        """Stream all frames of `reader` through the stage into `writer`.
+        ``emit(k_global, n)`` -> list of (batch-local index) to write for input frame k
+        (fps maps duplicate / drop frames on the host); default: each frame once."""
+        B = self.batch
+        rq = queue.Queue(maxsize=2)   # (slot, n) filled buffers
+        free_in = queue.Queue()
+        for i in range(2):
+            free_in.put(i)
+        err = []
+
+        def read_loop():
+            try:
+                while True:
+                    slot = free_in.get()
+                    n = reader.read_into(self.h_in[slot].numpy(), B)
+                    rq.put((slot, n))
+                    if n < B:
+                        return
+            except Exception as e:  # surface reader failures in the main thread
+                err.append(e)
+                rq.put((None, 0))
+
+        wq = queue.Queue(maxsize=2)
+
+        def write_loop():
+            try:
+                while True:
+                    item = wq.get()
+                    if item is None:
+                        return
+                    slot, n, ev, base = item
+                    ev.synchronize()
+                    buf = self.h_out[slot].numpy()
+                    if emit is None:
+                        writer.write(buf[:n])
+                    else:
+                        for i in range(n):
+                            for _ in range(emit(base + i)):
+                                writer.write(buf[i:i + 1])
+                    self.frames_out += n
+                    out_free[slot].set()
+            except Exception as e:
+                err.append(e)
+
+        out_free = [threading.Event(), threading.Event()]
+        for e in out_free:
+            e.set()
+        tr = threading.Thread(target=read_loop, daemon=True)
+        tw = threading.Thread(target=write_loop, daemon=True)
+        tr.start()
+        tw.start()
+        base = 0
+        while True:
+            slot, n = rq.get()
+            if slot is None or n == 0:
+                if slot is not None:
+                    free_in.put(slot)
+                break
+            out_free[slot].wait()
+            out_free[slot].clear()
+            with torch.cuda.stream(self.copy_stream):
+                self.d_in[slot].storage[:n].copy_(self.h_in[slot][:n], non_blocking=True)
+                h2d_done = torch.cuda.Event()
+                h2d_done.record(self.copy_stream)
+            self.compute_stream.wait_event(h2d_done)
+            with torch.cuda.stream(self.compute_stream):
+                src = FrameBatch.interleaved(self.stage.in_fmt, self.stage.in_w, self.stage.in_h, n,
+                                             device=self.device, storage=self.d_in[slot].storage[:n])
+                dst = FrameBatch.interleaved(self.stage.out_fmt, self.stage.out_w, self.stage.out_h, n,
+                                             device=self.device, storage=self.d_out[slot].storage[:n])
+                self.stage.process(src, dst, self.compute_stream)
+                comp_done = torch.cuda.Event()
+                comp_done.record(self.compute_stream)
+            self.copy_stream.wait_event(comp_done)
+            with torch.cuda.stream(self.copy_stream):
+                self.h_out[slot][:n].copy_(self.d_out[slot].storage[:n], non_blocking=True)
+                d2h_done = torch.cuda.Event()
+                d2h_done.record(self.copy_stream)
+            # the input slot can be refilled once its H2D copy has finished
+            h2d_done.synchronize()
+            free_in.put(slot)
+            wq.put((slot, n, d2h_done, base))
+            self.frames_in += n
+            base += n
+            if n < B:
+                break
+        wq.put(None)
+        tw.join()
+        tr.join(timeout=1.0)
+        if err:
+            raise err[0]
+        return self.frames_in

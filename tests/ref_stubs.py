@@ -141,9 +141,10 @@ class Pvs:
 
 
 def build(sc, root, pvs_methods):
-    """Scenario dict -> (test_config, pvs, post_processing).  ``pvs_methods`` is a
-    module/namespace providing get_pix_fmt_for_avpvs(pvs) and
-    get_vcodec_and_pix_fmt_for_cpvs(pvs, rawvideo) -- the reference's or pixpath's."""
+    """Scenario dict -> (test_config, pvs, post_processings).  ``pvs_methods``
+    provides get_pix_fmt_for_avpvs(pvs), get_vcodec_and_pix_fmt_for_cpvs(pvs,
+    rawvideo), get_buff_events_media_time(pvs) and hrc_get_buff_events_media_time(hrc)
+    -- the reference's (fixture generation) or pixpath's (tests)."""
     pps = [PostProcessing(*p) for p in sc["pps"]]
     tc = TestConfig(root, sc.get("type", "short"), pps)
     src = Src(tc, sc["src"][0], sc["src"][1], sc.get("src_pix_fmt", "yuv420p"), sc.get("src_fps", 60))
@@ -154,6 +155,7 @@ def build(sc, root, pvs_methods):
         segs.append(Segment(tc, src, ql, i, t, dur, sc["target_pix_fmt"]))
         t += dur
     hrc = Hrc(sc.get("events", [("quality_level", segs[0].duration)]))
+    hrc.get_buff_events_media_time = types.MethodType(pvs_methods.hrc_get_buff_events_media_time, hrc)
     pvs = Pvs(tc, sc.get("pvs_id", "P2SXM00_SRC001_HRC001"), src, hrc, segs)
     pvs.get_pix_fmt_for_avpvs = types.MethodType(pvs_methods.get_pix_fmt_for_avpvs, pvs)
     pvs.get_vcodec_and_pix_fmt_for_cpvs = types.MethodType(pvs_methods.get_vcodec_and_pix_fmt_for_cpvs, pvs)

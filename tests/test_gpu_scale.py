@@ -33,6 +33,11 @@ CASES = [
     (po.YUV422P, 1920, 1080, po.UYVY422, 1920, 1080, po.SWS_BICUBIC, "noise"),          # a5 interleave
     (po.YUV420P, 1920, 1080, po.UYVY422, 1920, 1080, po.SWS_BICUBIC, "noise"),          # a5 generic packed
     (po.YUV420P10LE, 640, 360, po.UYVY422, 640, 360, po.SWS_BICUBIC, "noise"),
+    (po.YUV420P, 3840, 2160, po.YUV420P, 640, 360, po.SWS_BICUBIC, "smooth"),          # 6x downscale (narrow strips)
+    (po.YUV422P10LE, 3840, 2160, po.YUV422P10LE, 960, 540, po.SWS_LANCZOS, "noise"),   # 4x lanczos (24+ taps)
+    (po.YUV420P, 640, 360, po.YUV420P, 3840, 2160, po.SWS_BICUBIC, "noise"),           # 6x upscale
+    (po.YUV422P10LE, 1920, 1080, po.YUV422P10LE, 1920, 1080, po.SWS_LANCZOS, "noise"), # identity size
+    (po.YUV420P, 8, 8, po.YUV420P, 3, 3, po.SWS_BICUBIC, "noise"),                     # tiny
 ]
 
 

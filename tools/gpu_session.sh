@@ -1,11 +1,16 @@
+# One GPU session: parity tests, bench, rocprof kernel trace + PMC passes.
+# Usage (through gpurun): bash tools/gpu_session.sh TAG
 set -o pipefail
+TAG=${1:-run}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu_r1c.log 2>&1; echo "pytest rc=$?"
-grep -E "passed|failed" gpurun_out/pytest_gpu_r1c.log | tail -3
-timeout -k 10 300 python bench.py > gpurun_out/bench_r1a.json 2> gpurun_out/bench_r1a.err && cat gpurun_out/bench_r1a.json &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof_kt.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > gpurun_out/prof_fetch.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > gpurun_out/prof_write.log 2>&1
+timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu_$TAG.log 2>&1; echo "pytest rc=$?"
+grep -E "passed|failed" gpurun_out/pytest_gpu_$TAG.log | tail -3
+grep -E "^FAILED" gpurun_out/pytest_gpu_$TAG.log | head -20
+timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err && cat gpurun_out/bench_$TAG.json &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt_$TAG -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof_kt_$TAG.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch_$TAG -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > gpurun_out/prof_fetch_$TAG.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_$TAG -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > gpurun_out/prof_write_$TAG.log 2>&1 &&
+python3 tools/pmc_traffic.py gpurun_out/prof_fetch_$TAG/run_counter_collection.csv gpurun_out/prof_write_$TAG/run_counter_collection.csv gpurun_out/prof_kt_$TAG/run_kernel_trace.csv gpurun_out/pmc_traffic_$TAG.json 600 > /dev/null &&
+cat gpurun_out/prof_kt_$TAG/run_kernel_stats.csv | cut -c1-160
 echo "final rc=$?"
-find gpurun_out -name "*.csv" | head -20
