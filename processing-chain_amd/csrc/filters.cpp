@@ -201,16 +201,19 @@ int FilterBank::compact(int src_n, int bucket_min, Compact *out, std::string *er
     }
     int taps = span;
     if (taps < bucket_min) taps = bucket_min;
-    if (taps > src_n) {
+    if (span > src_n) {
         *err = "source plane narrower than the filter";
         return -1;
     }
+    // a window wider than the plane (tiny planes, bucketed taps) starts at 0; the
+    // kernel's staging zero-fills samples past the plane edge
     out->taps = taps;
     out->pos.assign(n, 0);
     out->coef.assign(static_cast<size_t>(n) * taps, 0);
     for (int i = 0; i < n; ++i) {
         int start = pos[i] + lo[i];
         if (start + taps > src_n) start = src_n - taps;  // window slides left, leading zeros
+        if (start < 0) start = 0;
         out->pos[i] = start;
         const int16_t *c = &coef[static_cast<size_t>(i) * size];
         for (int j = 0; j < size; ++j) {

@@ -97,6 +97,48 @@ __device__ inline void stage_chunk(uint16_t *lds_dst, const ST *g, int col, int 
     }
 }
 
+// Register prefetch of up to kPF 16-byte source chunks per lane (software
+// pipelining of the staging: issued before the vertical pass of the previous
+// chunk, committed to LDS after it).
+constexpr int kPF = 4;
+
+template <typename ST>
+struct Prefetch {
+    uint4 v[kPF];
+};
+
+template <typename ST>
+__device__ inline uint4 load16(const ST *g, int col, int sw, bool vec) {
+    constexpr int CH = 16 / sizeof(ST);
+    if (vec && col + CH <= sw) return *reinterpret_cast<const uint4 *>(g + col);
+    uint4 r = {0, 0, 0, 0};
+    ST tmp[CH];
+#pragma unroll
+    for (int e = 0; e < CH; ++e) tmp[e] = (col + e < sw) ? g[col + e] : ST(0);
+    __builtin_memcpy(&r, tmp, 16);
+    return r;
+}
+
+template <typename ST>
+__device__ inline void store16(uint16_t *lds_dst, uint4 v) {
+    if constexpr (sizeof(ST) == 2) {
+        *reinterpret_cast<uint4 *>(lds_dst) = v;
+    } else {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint4 lo, hi;
+        lo.x = __builtin_amdgcn_perm(0, w[0], 0x0c010c00u);
+        lo.y = __builtin_amdgcn_perm(0, w[0], 0x0c030c02u);
+        lo.z = __builtin_amdgcn_perm(0, w[1], 0x0c010c00u);
+        lo.w = __builtin_amdgcn_perm(0, w[1], 0x0c030c02u);
+        hi.x = __builtin_amdgcn_perm(0, w[2], 0x0c010c00u);
+        hi.y = __builtin_amdgcn_perm(0, w[2], 0x0c030c02u);
+        hi.z = __builtin_amdgcn_perm(0, w[3], 0x0c010c00u);
+        hi.w = __builtin_amdgcn_perm(0, w[3], 0x0c030c02u);
+        reinterpret_cast<uint4 *>(lds_dst)[0] = lo;
+        reinterpret_cast<uint4 *>(lds_dst)[1] = hi;
+    }
+}
+
 template <typename ST, int OUTB, int HT>
 __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     extern __shared__ __align__(16) uint16_t lds[];
@@ -114,6 +156,8 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     const int S = J.S, mask = J.ring - 1;
     uint16_t *src_t = lds;                                              // [maxnew][S]
     int16_t *ring = reinterpret_cast<int16_t *>(lds + J.maxnew * S);    // [ring][TW]
+    int16_t *vcl = ring + J.ring * TW;                                   // [cho][vt] chunk V taps
+    int32_t *vpl = reinterpret_cast<int32_t *>(vcl + ((J.cho * J.vt + 1) & ~1)); // [cho] chunk V rows
     const int tid = threadIdx.x;
     const ST *sbase = reinterpret_cast<const ST *>(a.src[p] + frame * a.sfs[p]);
     uint8_t *dbase = a.dst[p] + frame * a.dfs[p];
@@ -135,28 +179,67 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     const int vt = J.vt;
 
     const int y_begin = seg * J.seg_h, y_end = min(J.dh, y_begin + J.seg_h);
+    constexpr int CH = 16 / sizeof(ST);
+    const int cpr = (cn + CH - 1) / CH;  // 16-B chunks per staged row
+    const int64_t sls = a.sls[p];
+    const bool vec = a.vec_src;
+    const int sw = J.sw;
+    // issue the loads of chunk rows [from, hi) for this lane (first kPF * 256 chunks)
+    auto prefetch = [&](Prefetch<ST> &pf, int from, int hi_) {
+        const int total = (hi_ - from) * cpr;
+#pragma unroll
+        for (int k = 0; k < kPF; ++k) {
+            const int id = tid + k * kThreads;
+            if (id < total) {
+                const int r = id / cpr, ch = id - r * cpr;
+                const ST *g = reinterpret_cast<const ST *>(reinterpret_cast<const uint8_t *>(sbase) +
+                                                           (int64_t)(from + r) * sls);
+                pf.v[k] = load16<ST>(g, c0 + ch * CH, sw, vec);
+            }
+        }
+    };
+    // write the prefetched chunks to LDS and stage any remainder synchronously
+    auto commit = [&](const Prefetch<ST> &pf, int from, int hi_) {
+        const int total = (hi_ - from) * cpr;
+#pragma unroll
+        for (int k = 0; k < kPF; ++k) {
+            const int id = tid + k * kThreads;
+            if (id < total) {
+                const int r = id / cpr, ch = id - r * cpr;
+                store16<ST>(src_t + r * S + ch * CH, pf.v[k]);
+            }
+        }
+        for (int id = tid + kPF * kThreads; id < total; id += kThreads) {
+            const int r = id / cpr, ch = id - r * cpr;
+            const ST *g = reinterpret_cast<const ST *>(reinterpret_cast<const uint8_t *>(sbase) +
+                                                       (int64_t)(from + r) * sls);
+            store16<ST>(src_t + r * S + ch * CH, load16<ST>(g, c0 + ch * CH, sw, vec));
+        }
+    };
+
     int next_src = J.chunk_lo[y_begin / J.cho];
+    Prefetch<ST> pf;
+    // rows the first chunk needs
+    int pf_from = next_src, pf_hi = J.chunk_hi[y_begin / J.cho];
+    if (pf_from < J.chunk_lo[y_begin / J.cho]) pf_from = J.chunk_lo[y_begin / J.cho];
+    prefetch(pf, pf_from, pf_hi);
     for (int y0 = y_begin; y0 < y_end; y0 += J.cho) {
         const int ci = y0 / J.cho;
         const int lo = J.chunk_lo[ci], hi = J.chunk_hi[ci];
         if (next_src < lo) next_src = lo;
         const int nnew = hi - next_src;
-        // ---- stage the new source rows [next_src, hi) -----------------------
-        if (nnew > 0) {
-            constexpr int CH = 16 / sizeof(ST);
-            const int cpr = (cn + CH - 1) / CH;
-            const int total = nnew * cpr;
-            for (int id = tid; id < total; id += kThreads) {
-                const int r = id / cpr, ch = id - r * cpr;
-                const ST *g = reinterpret_cast<const ST *>(reinterpret_cast<const uint8_t *>(sbase) +
-                                                           (int64_t)(next_src + r) * a.sls[p]);
-                stage_chunk<ST>(src_t + r * S + ch * CH, g, c0 + ch * CH, J.sw, a.vec_src);
-            }
+        // ---- stage the chunk's vertical taps/rows and commit the prefetched rows ----
+        {
+            const int ny_c = min(J.cho, y_end - y0);
+            for (int i = tid; i < ny_c * J.vt; i += kThreads) vcl[i] = J.vcoef[(int64_t)y0 * J.vt + i];
+            for (int i = tid; i < ny_c; i += kThreads) vpl[i] = J.vpos[y0 + i];
         }
+        if (nnew > 0) commit(pf, next_src, hi);
         __syncthreads();  // staged rows visible; the previous chunk's vertical pass is done
         // ---- horizontal pass into the ring --------------------------------------
         if (nnew > 0 && col < nx) {
             const uint16_t *s = src_t + r_first * S + hoff;
+#pragma unroll 4
             for (int r = r_first; r < nnew; r += r_step) {
                 int acc = 0;
 #pragma unroll
@@ -168,6 +251,11 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
         }
         if (nnew > 0) next_src = hi;
         __syncthreads();
+        // ---- prefetch the next chunk's new rows; their loads overlap the V pass ----
+        if (y0 + J.cho < y_end) {
+            const int nlo = J.chunk_lo[ci + 1], nhi = J.chunk_hi[ci + 1];
+            prefetch(pf, max(next_src, nlo), nhi);
+        }
         // ---- vertical pass: output rows [y0, y0 + cho) --------------------------
         const int ny = min(J.cho, y_end - y0);
         for (int yy0 = row_first; yy0 < ny + row_first; yy0 += row_step) {
@@ -175,10 +263,11 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
             if (TW == kTileW) yy = __builtin_amdgcn_readfirstlane(yy);
             if (yy >= ny) break;
             const int y = y0 + yy;
-            const int vp = J.vpos[y];
-            const int16_t *vc = J.vcoef + (int64_t)y * vt;
+            const int vp = vpl[yy];
+            const int16_t *vc = vcl + yy * vt;
             if (cx >= nx) continue;
             int acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
+#pragma unroll 4
             for (int k = 0; k < vt; ++k) {
                 const int cf = vc[k];
                 const uint2 q = *reinterpret_cast<const uint2 *>(ring + ((vp + k) & mask) * TW + cx);
@@ -401,7 +490,8 @@ int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::
             nseg = (dh + seg_h - 1) / seg_h;
             int maxnew, ring;
             row_chunks(hp, sh, dh, cho, seg_h, &maxnew, &ring);
-            const size_t bytes = (size_t)maxnew * S * 2 + (size_t)ring * tw * 2;
+            const size_t bytes = (size_t)maxnew * S * 2 + (size_t)ring * tw * 2 +
+                                 (size_t)((cho * hp.v.taps + 1) & ~1) * 2 + (size_t)cho * 4;
             if (bytes > (size_t)pp::kLdsBudget) continue;
             hp.tiles_x = (dw + tw - 1) / tw;
             hp.nseg = nseg; hp.tw = tw; hp.seg_h = seg_h; hp.cho = cho;

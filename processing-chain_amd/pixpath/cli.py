@@ -212,7 +212,9 @@ def stall_schedule(buffer_events, rate, n_in, skipping, spinner_delays=None, bla
             for i in range(a, b):
                 seq[i] = (max(a - 1, 0), -1)
         return seq
-    delays = list(spinner_delays) if spinner_delays is not None else [0.0]
+    # exact rational clock: APNG delays are num/den fractions
+    delays = [Fraction(float(d)).limit_denominator(100000) for d in
+              (spinner_delays if spinner_delays is not None else [0.0])]
     period = sum(delays)
     out, cursor = [], 0
     for t, d in sorted(buffer_events):
@@ -222,8 +224,8 @@ def stall_schedule(buffer_events, rate, n_in, skipping, spinner_delays=None, bla
         frozen = at - 1 if at > 0 else (-1 if black_frame else 0)
         k = int(round(d * rate))
         for j in range(k):
-            ts = (j / float(rate)) % period if period > 0 else 0.0
-            acc, si = 0.0, 0
+            ts = (Fraction(j) / rate) % period if period > 0 else Fraction(0)
+            acc, si = Fraction(0), 0
             for si, dl in enumerate(delays):
                 acc += dl
                 if ts < acc:

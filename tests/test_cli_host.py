@@ -1,0 +1,71 @@
+"""Host-side pieces of the GPU pipeline (CPU): Y4M/raw I/O, stall schedule
+(PP-STALL-1), fps duplication counts == the vf_fps map."""
+import numpy as np
+import pytest
+
+import pyoracle as po
+import synth
+from pixpath import chain, io as pio
+from pixpath.cli import _fps_counts, stall_schedule
+
+
+def test_y4m_roundtrip(tmp_path):
+    rng = np.random.default_rng(0)
+    frames = [synth.noise_frame(rng, po.YUV422P10LE, 48, 20) for _ in range(3)]
+    raw = pio.join_planes(synth.batch(frames))
+    p = str(tmp_path / "a.y4m")
+    w = pio.Y4MWriter(p, "yuv422p10le", 48, 20, "60000/1001")
+    w.write(raw)
+    w.close()
+    r = pio.open_reader(p)
+    assert (r.w, r.h, r.fmt.name, r.rate) == (48, 20, "yuv422p10le", pio.Fraction(60000, 1001))
+    got = list(r.batches(2))
+    assert [g[0].shape[0] for g in got] == [2, 1]
+    back = [np.concatenate([g[i] for g in got]) for i in range(3)]
+    for a, b in zip(back, synth.batch(frames)):
+        np.testing.assert_array_equal(a, b)
+    assert pio.probe(p)["stream"]["pix_fmt"] == "yuv422p10le"
+
+
+def test_split_join_planes():
+    rng = np.random.default_rng(1)
+    fr = synth.batch([synth.noise_frame(rng, po.YUV420P, 30, 14) for _ in range(2)])
+    raw = pio.join_planes(fr)
+    for a, b in zip(pio.split_planes(raw, "yuv420p", 30, 14), fr):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("a,b,n", [(30, 60, 17), (24, 60, 33), (60, 30, 20), (60, 60, 9), (25, 60, 50),
+                                   ("30000/1001", 60, 31)])
+def test_fps_counts_match_map(a, b, n):
+    counts = _fps_counts(a, b)
+    m = chain.fps_index_map(n, a, b)
+    expanded = [i for i in range(n) for _ in range(counts(i))]
+    assert expanded == m
+
+
+def test_stall_schedule_spinner():
+    # AVPVS 6 s @ 10 fps, stalls [[2, 1.5], [4, 1.0]] (media time), spinner 8 x 0.25 s
+    seq = stall_schedule([[2, 1.5], [4, 1.0]], 10, 60, False, [0.25] * 8)
+    assert len(seq) == 60 + 15 + 10
+    assert seq[:20] == [(i, -1) for i in range(20)]
+    stall1 = seq[20:35]
+    assert all(s == 19 for s, _ in stall1)
+    assert [sp for _, sp in stall1] == [0, 0, 0, 1, 1, 2, 2, 2, 3, 3, 4, 4, 4, 5, 5]
+    assert seq[35:55] == [(i, -1) for i in range(20, 40)]
+    assert all(s == 39 and sp >= 0 for s, sp in seq[55:65])
+    assert seq[65:] == [(i, -1) for i in range(40, 60)]
+
+
+def test_stall_at_zero_is_black():
+    seq = stall_schedule([[0, 0.5]], 10, 4, False, [0.1] * 8, black_frame=True)
+    assert seq[:5] == [(-1, k) for k in range(5)] and seq[5:] == [(i, -1) for i in range(4)]
+    seq = stall_schedule([[0, 0.5]], 10, 4, False, [0.1] * 8, black_frame=False)
+    assert seq[0] == (0, 0)
+
+
+def test_freeze_with_skipping_keeps_length():
+    seq = stall_schedule([[1, 0.5], [3, 0.2]], 10, 50, True)
+    assert len(seq) == 50
+    assert seq[10:15] == [(9, -1)] * 5 and seq[15] == (15, -1)
+    assert seq[30:32] == [(29, -1)] * 2
