@@ -118,6 +118,16 @@ int pp_pad_execute(pp_ctx *ctx, int fmt, int src_w, int src_h,
 int pp_v210_pack(pp_ctx *ctx, int w, int h, const pp_frames *src,
                  const pp_frames *dst, int nframes, void *stream);
 
+/* Fused PC CPVS: `fps,pad=W:H:(ow-iw)/2:(oh-ih)/2` + `-pix_fmt` conversion +
+ * packing in one pass (lib/ffmpeg.py:1177-1201).  src: AVPVS frames (w x h,
+ * yuv420p/yuv422p for out_fmt PP_FMT_UYVY422, yuv420p10le/yuv422p10le for
+ * PP_FMT_V210); canvas W x H with the input at (x, y) (-1 = centred, rounded
+ * to the chroma grid); dst plane 0, 16-B aligned.  Bit-identical to pad ->
+ * swscale (bicubic) -> packer. */
+int pp_cpvs_execute(pp_ctx *ctx, int src_fmt, int w, int h, const pp_frames *src,
+                    int W, int H, int x, int y, int out_fmt,
+                    const pp_frames *dst, int nframes, void *stream);
+
 /* ---- stall compositing (spec PP-STALL-1) -----------------
  * Replaces the external `bufferer -s spinner.png` call at
  * p03_generateAvPvs.py:236-243.  Uploads one spinner animation (n RGBA8

@@ -147,9 +147,15 @@ def cmd_cpvs(args):
     W, H = int(W), int(H)
     cur_fmt = rd.fmt
     steps = []
-    if args.pad:
+    fused = (args.vcodec == "rawvideo" and args.pix_fmt == "uyvy422" and cur_fmt.depth == 8) or \
+            (args.vcodec == "v210" and cur_fmt.depth == 10)
+    if fused:  # one pass: pad + chroma conversion + packing (pp_cpvs_execute)
+        steps.append(("cpvs",))
+    elif args.pad:
         steps.append(("pad", W, H))
-    if args.vcodec == "rawvideo" and args.pix_fmt == "uyvy422":
+    if fused:
+        out_fmt = formats.fmt("uyvy422" if cur_fmt.depth == 8 else "v210")
+    elif args.vcodec == "rawvideo" and args.pix_fmt == "uyvy422":
         out_fmt = formats.fmt("uyvy422")
         steps.append(("scale", ops.Scaler(cur_fmt, W, H, "uyvy422", W, H, flags="bicubic")))
     elif args.vcodec == "v210":
@@ -171,7 +177,10 @@ def cmd_cpvs(args):
         cur = src
         for i, st in enumerate(steps):
             last = i == len(steps) - 1
-            if st[0] == "pad":
+            if st[0] == "cpvs":
+                nxt = dst
+                ops.cpvs(cur, W, H, out_fmt, dst=nxt, stream=stream)
+            elif st[0] == "pad":
                 nxt = dst if last else tmp("pad", cur.fmt, cur.n, cur.device)
                 ops.pad(cur, W, H, dst=nxt, stream=stream)
             elif st[0] == "scale":

@@ -130,6 +130,23 @@ def v210_pack(src, dst=None, stream=None):
     return dst
 
 
+def cpvs(src, W=None, H=None, out_fmt=None, x=-1, y=-1, dst=None, stream=None):
+    """Fused PC CPVS: pad to W x H (reference centring) + 4:2:0->4:2:2 + uyvy422
+    (8-bit AVPVS) or v210 (10-bit) packing in one pass (lib/ffmpeg.py:1177-1201)."""
+    W = src.w if W is None else int(W)
+    H = src.h if H is None else int(H)
+    if out_fmt is None:
+        out_fmt = formats.UYVY422 if src.fmt.depth == 8 else formats.V210
+    of = formats.fmt(out_fmt)
+    ctx = context(src.device.index)
+    if dst is None:
+        dst = FrameBatch(of, W, H, src.n, device=src.device)
+    s, d = src.frames_struct(), dst.frames_struct()
+    check(lib().pp_cpvs_execute(ctx.handle, src.fmt.id, src.w, src.h, ctypes.byref(s), W, H, x, y, of.id,
+                                ctypes.byref(d), src.n, _stream(src.planes[0], stream)))
+    return dst
+
+
 def siti(luma, bitdepth, prev=None, stream=None):
     """Per-frame P.910 SI/TI of a [N, H, W] luma tensor (uint8 / uint16, may be a
     pitched view).  Returns two float64 device tensors [N]; ti[0] is NaN when

@@ -71,3 +71,28 @@ def test_stall_compose_matches_oracle(gpu, fmt):
         ref = base if sp_idx[k] < 0 else po.overlay_spinner(fmt, base, po.spinner_to_yuva(anim[sp_idx[k]], fmt))
         for p in range(3):
             np.testing.assert_array_equal(out[p][k], ref[p], err_msg="frame %d plane %d" % (k, p))
+
+
+@pytest.mark.parametrize("fmt,w,h,W,H", [
+    (po.YUV420P, 1920, 800, 1920, 1080), (po.YUV420P, 1920, 1080, 1920, 1080), (po.YUV422P, 1920, 1012, 1920, 1080),
+    (po.YUV420P10LE, 1920, 1080, 1920, 1080), (po.YUV420P10LE, 1920, 800, 1920, 1080),
+    (po.YUV422P10LE, 1920, 1080, 1920, 1080), (po.YUV422P10LE, 1280, 534, 1280, 720), (po.YUV420P10LE, 100, 38, 100, 50),
+    (po.YUV420P, 102, 38, 102, 50),
+])
+def test_fused_cpvs_matches_chain(gpu, fmt, w, h, W, H):
+    """pp_cpvs_execute == pad -> swscale (bicubic, -> uyvy422 / yuv422p10le) -> v210, bit-exact."""
+    from pixpath import ops
+    from pixpath.frames import FrameBatch
+    rng = np.random.default_rng(8)
+    frames = [synth.noise_frame(rng, fmt, w, h) for _ in range(2)]
+    src = FrameBatch.from_numpy(fmt, synth.batch(frames), device=gpu)
+    out = ops.cpvs(src, W, H).to_numpy()[0]
+    depth = po.fmt_info(fmt)[0]
+    for i in range(2):
+        padded = po.pad(fmt, frames[i], W, H, (W - w) // 2, (H - h) // 2)
+        if depth == 8:
+            (ref,) = po.scale(fmt, padded, po.UYVY422, W, H)
+        else:
+            p422 = padded if fmt == po.YUV422P10LE else po.scale(fmt, padded, po.YUV422P10LE, W, H)
+            ref = po.v210_pack(p422)
+        np.testing.assert_array_equal(out[i], ref)
