@@ -44,13 +44,13 @@ __constant__ uint8_t c_dither[8][8] = {
 struct PlaneJob {
     int sw, sh, dw, dh;
     int tiles_x, tiles_y, tile_base;  // strips x vertical segments, first block index
-    int tw, seg_h, cho;   // strip width, output rows per segment, output rows per chunk
-    int vt, ring, maxnew, S; // V taps, ring rows (pow2), staged rows per chunk, staged cols
+    int tw, twl, seg_h, cho; // strip width (= 1 << twl), output rows per segment, output rows per chunk
+    int vtp, ring, maxnew, S; // V tap pairs, ring rows (pow2, >= 2), staged rows per chunk, staged cols
     int dither_off;       // 0 (Y, U) or 3 (V)
     const int32_t *hpos;  // [dw]   window start (absolute source column)
     const int16_t *hcoef; // [dw * HT]
-    const int32_t *vpos;  // [dh]
-    const int16_t *vcoef; // [dh * vt]
+    const int32_t *vbase; // [dh]   first ring row of the window, rounded down to even
+    const int32_t *vcoef2; // [dh * vtp] tap pairs (rows base+2j, base+2j+1) packed lo|hi
     const int32_t *tile_c0, *tile_cn; // [tiles_x] staged column window per strip
     const int32_t *chunk_lo, *chunk_hi; // [ceil(dh/cho)] source rows needed by each chunk
 };
@@ -68,35 +68,6 @@ struct ScaleArgs {
     int vec_dst;  // all destination rows 8-B aligned (4 outputs per lane)
 };
 
-template <typename ST>
-__device__ inline void stage_chunk(uint16_t *lds_dst, const ST *g, int col, int sw, bool vec) {
-    // 16 bytes of source -> 8 (u16) or 16 (u8) LDS samples
-    constexpr int CH = 16 / sizeof(ST);
-    if (vec && col + CH <= sw) {
-        if constexpr (sizeof(ST) == 2) {
-            *reinterpret_cast<uint4 *>(lds_dst) = *reinterpret_cast<const uint4 *>(g + col);
-        } else {
-            const uint4 v = *reinterpret_cast<const uint4 *>(g + col);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            uint4 lo, hi;
-            // widen 16 bytes to 16 u16 (byte permutes, no per-byte shifts)
-            lo.x = __builtin_amdgcn_perm(0, w[0], 0x0c010c00u);
-            lo.y = __builtin_amdgcn_perm(0, w[0], 0x0c030c02u);
-            lo.z = __builtin_amdgcn_perm(0, w[1], 0x0c010c00u);
-            lo.w = __builtin_amdgcn_perm(0, w[1], 0x0c030c02u);
-            hi.x = __builtin_amdgcn_perm(0, w[2], 0x0c010c00u);
-            hi.y = __builtin_amdgcn_perm(0, w[2], 0x0c030c02u);
-            hi.z = __builtin_amdgcn_perm(0, w[3], 0x0c010c00u);
-            hi.w = __builtin_amdgcn_perm(0, w[3], 0x0c030c02u);
-            reinterpret_cast<uint4 *>(lds_dst)[0] = lo;
-            reinterpret_cast<uint4 *>(lds_dst)[1] = hi;
-        }
-    } else {
-#pragma unroll
-        for (int e = 0; e < CH; ++e) lds_dst[e] = (col + e < sw) ? static_cast<uint16_t>(g[col + e]) : 0;
-    }
-}
-
 // Register prefetch of up to kPF 16-byte source chunks per lane (software
 // pipelining of the staging: issued before the vertical pass of the previous
 // chunk, committed to LDS after it).
@@ -107,10 +78,10 @@ struct Prefetch {
     uint4 v[kPF];
 };
 
+// Unaligned-source fallback: element loads, zero past the plane edge.
 template <typename ST>
-__device__ inline uint4 load16(const ST *g, int col, int sw, bool vec) {
+__device__ inline uint4 load16_scalar(const ST *g, int col, int sw) {
     constexpr int CH = 16 / sizeof(ST);
-    if (vec && col + CH <= sw) return *reinterpret_cast<const uint4 *>(g + col);
     uint4 r = {0, 0, 0, 0};
     ST tmp[CH];
 #pragma unroll
@@ -119,9 +90,28 @@ __device__ inline uint4 load16(const ST *g, int col, int sw, bool vec) {
     return r;
 }
 
+// Bounds-checked 16-B load through the frame plane's buffer resource: bytes at
+// or past num_records read as 0 without touching memory, so lanes with no
+// chunk (and the right edge of the plane's last row) need no branch.  Samples
+// past a row's end inside the plane come from the next row; the compacted
+// filters give them zero weight.
+__device__ inline uint4 bload16(__amdgpu_buffer_rsrc_t rs, int off) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    uint4 r;
+    __builtin_memcpy(&r, &v, 16);
+    return r;
+}
+constexpr int kOobOff = 0x7ffffff0;  // any offset >= num_records
+
+typedef int16_t v2i16 __attribute__((ext_vector_type(2)));
+
+// 16-bit sources are stored as s ^ 0x8000 (= s - 32768 as int16) so any u16
+// sample is an exact signed operand of v_dot2_i32_i16; the H pass adds the
+// 32768 * sum(coef) bias back.  8-bit samples are stored as-is (<= 255).
 template <typename ST>
 __device__ inline void store16(uint16_t *lds_dst, uint4 v) {
     if constexpr (sizeof(ST) == 2) {
+        v.x ^= 0x80008000u; v.y ^= 0x80008000u; v.z ^= 0x80008000u; v.w ^= 0x80008000u;
         *reinterpret_cast<uint4 *>(lds_dst) = v;
     } else {
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -155,28 +145,47 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     const int c0 = J.tile_c0[tx], cn = J.tile_cn[tx];
     const int S = J.S, mask = J.ring - 1;
     uint16_t *src_t = lds;                                              // [maxnew][S]
-    int16_t *ring = reinterpret_cast<int16_t *>(lds + J.maxnew * S);    // [ring][TW]
-    int16_t *vcl = ring + J.ring * TW;                                   // [cho][vt] chunk V taps
-    int32_t *vpl = reinterpret_cast<int32_t *>(vcl + ((J.cho * J.vt + 1) & ~1)); // [cho] chunk V rows
+    // ring of 15-bit intermediates, row pairs interleaved per column:
+    // element (row R, col c) at [((R & mask) >> 1) * TW + c] * 2 + (R & 1)
+    int16_t *ring = reinterpret_cast<int16_t *>(lds + J.maxnew * S);
+    int32_t *vcl = reinterpret_cast<int32_t *>(ring + J.ring * TW);     // [cho][vtp] chunk V tap pairs
+    int32_t *vpl = vcl + J.cho * J.vtp;                                  // [cho] chunk V base rows
     const int tid = threadIdx.x;
     const ST *sbase = reinterpret_cast<const ST *>(a.src[p] + frame * a.sfs[p]);
     uint8_t *dbase = a.dst[p] + frame * a.dfs[p];
 
     // horizontal-pass lane mapping: one output column per lane, r_step rows at a time
     const int col = tid % TW, r_first = tid / TW, r_step = kThreads / TW;
-    int hc[HT];
+    // taps as packed 16-bit pairs for v_dot2_i32_i16 (HT is 1 or even)
+    constexpr int HP = HT == 1 ? 1 : HT / 2;
+    v2i16 hcp[HP];
+    int hbias = 0;  // 32768 * sum(coef): undoes the staging bias of 16-bit samples
     int hoff = 0;
     if (col < nx) {
         const int x = x0 + col;
         hoff = J.hpos[x] - c0;
+        int hsum = 0;
+        if constexpr (HT == 1) {
+            const int c = J.hcoef[x];
+            hcp[0] = v2i16{(int16_t)c, 0};
+            hsum = c;
+        } else {
 #pragma unroll
-        for (int k = 0; k < HT; ++k) hc[k] = J.hcoef[(int64_t)x * HT + k];
+            for (int j = 0; j < HP; ++j) {
+                const int16_t c0_ = J.hcoef[(int64_t)x * HT + 2 * j], c1_ = J.hcoef[(int64_t)x * HT + 2 * j + 1];
+                hcp[j] = v2i16{c0_, c1_};
+                hsum += c0_ + c1_;
+            }
+        }
+        if constexpr (sizeof(ST) == 2) hbias = hsum * 32768;
     }
     // vertical-pass lane mapping: 4 adjacent outputs per lane
     const int groups = TW / 4;
     const int lane_g = tid % groups, row_first = tid / groups, row_step = kThreads / groups;
     const int cx = lane_g * 4;
-    const int vt = J.vt;
+    const int vtp = J.vtp;
+    const int twl = J.twl;
+    const int rbytes_mask = (J.ring << (twl + 1)) - 1;  // ring bytes - 1
 
     const int y_begin = seg * J.seg_h, y_end = min(J.dh, y_begin + J.seg_h);
     constexpr int CH = 16 / sizeof(ST);
@@ -184,23 +193,35 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     const int64_t sls = a.sls[p];
     const bool vec = a.vec_src;
     const int sw = J.sw;
-    // issue the loads of chunk rows [from, hi) for this lane (first kPF * 256 chunks)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<ST *>(sbase), (short)0, (int)((int64_t)(J.sh - 1) * sls + (int64_t)sw * sizeof(ST)), 0x00020000);
+    const int cbyte = c0 * (int)sizeof(ST);
+    // byte offset of chunk `id` of rows [from, ...) (kOobOff when id >= total)
+    auto chunk_off = [&](int id, int from, int total) {
+        const int r = id / cpr, ch = id - r * cpr;
+        const int off = (from + r) * (int)sls + cbyte + ch * 16;
+        return id < total ? off : kOobOff;
+    };
+    // issue the loads of chunk rows [from, hi) for this lane (first kPF * 256
+    // chunks); straight-line code, so the kPF loads are all in flight at once
     auto prefetch = [&](Prefetch<ST> &pf, int from, int hi_) {
+        if (!vec) return;
         const int total = (hi_ - from) * cpr;
 #pragma unroll
-        for (int k = 0; k < kPF; ++k) {
-            const int id = tid + k * kThreads;
-            if (id < total) {
-                const int r = id / cpr, ch = id - r * cpr;
-                const ST *g = reinterpret_cast<const ST *>(reinterpret_cast<const uint8_t *>(sbase) +
-                                                           (int64_t)(from + r) * sls);
-                pf.v[k] = load16<ST>(g, c0 + ch * CH, sw, vec);
-            }
-        }
+        for (int k = 0; k < kPF; ++k) pf.v[k] = bload16(rs, chunk_off(tid + k * kThreads, from, total));
     };
     // write the prefetched chunks to LDS and stage any remainder synchronously
     auto commit = [&](const Prefetch<ST> &pf, int from, int hi_) {
         const int total = (hi_ - from) * cpr;
+        if (!vec) {
+            for (int id = tid; id < total; id += kThreads) {
+                const int r = id / cpr, ch = id - r * cpr;
+                const ST *g = reinterpret_cast<const ST *>(reinterpret_cast<const uint8_t *>(sbase) +
+                                                           (int64_t)(from + r) * sls);
+                store16<ST>(src_t + r * S + ch * CH, load16_scalar<ST>(g, c0 + ch * CH, sw));
+            }
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < kPF; ++k) {
             const int id = tid + k * kThreads;
@@ -211,9 +232,7 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
         }
         for (int id = tid + kPF * kThreads; id < total; id += kThreads) {
             const int r = id / cpr, ch = id - r * cpr;
-            const ST *g = reinterpret_cast<const ST *>(reinterpret_cast<const uint8_t *>(sbase) +
-                                                       (int64_t)(from + r) * sls);
-            store16<ST>(src_t + r * S + ch * CH, load16<ST>(g, c0 + ch * CH, sw, vec));
+            store16<ST>(src_t + r * S + ch * CH, bload16(rs, chunk_off(id, from, total)));
         }
     };
 
@@ -228,24 +247,42 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
         const int lo = J.chunk_lo[ci], hi = J.chunk_hi[ci];
         if (next_src < lo) next_src = lo;
         const int nnew = hi - next_src;
-        // ---- stage the chunk's vertical taps/rows and commit the prefetched rows ----
+        // ---- commit the prefetched rows (src_t is not read by the vertical pass) ----
+        if (nnew > 0) commit(pf, next_src, hi);
+        __syncthreads();  // staged rows visible; every wave has left the previous vertical pass
+        // ---- this chunk's vertical taps/rows: written only after the barrier above
+        // (the previous vertical pass reads them), visible after the one below ----
         {
             const int ny_c = min(J.cho, y_end - y0);
-            for (int i = tid; i < ny_c * J.vt; i += kThreads) vcl[i] = J.vcoef[(int64_t)y0 * J.vt + i];
-            for (int i = tid; i < ny_c; i += kThreads) vpl[i] = J.vpos[y0 + i];
+            for (int i = tid; i < ny_c * vtp; i += kThreads) vcl[i] = J.vcoef2[(int64_t)y0 * vtp + i];
+            for (int i = tid; i < ny_c; i += kThreads) vpl[i] = J.vbase[y0 + i];
         }
-        if (nnew > 0) commit(pf, next_src, hi);
-        __syncthreads();  // staged rows visible; the previous chunk's vertical pass is done
         // ---- horizontal pass into the ring --------------------------------------
         if (nnew > 0 && col < nx) {
-            const uint16_t *s = src_t + r_first * S + hoff;
+            // 4-B aligned dword reads (2-B aligned ones stall the LDS); an odd
+            // window start takes each sample pair from two dwords with v_alignbit
+            const int odd = hoff & 1;
+            const uint32_t ash = odd * 16;
+            const uint16_t *s = src_t + r_first * S + hoff - odd;
 #pragma unroll 4
             for (int r = r_first; r < nnew; r += r_step) {
-                int acc = 0;
+                int acc = hbias;
+                if constexpr (HT == 1) {
+                    acc += static_cast<int>(static_cast<int16_t>(s[odd])) * hcp[0][0];
+                } else {
+                    const uint32_t *sw32 = static_cast<const uint32_t *>(__builtin_assume_aligned(s, 4));
+                    uint32_t w[HP + 1];
 #pragma unroll
-                for (int k = 0; k < HT; ++k) acc += static_cast<int>(s[k]) * hc[k];
+                    for (int j = 0; j <= HP; ++j) w[j] = sw32[j];
+#pragma unroll
+                    for (int j = 0; j < HP; ++j)
+                        acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, __builtin_amdgcn_alignbit(w[j + 1], w[j], ash)),
+                                                     hcp[j], acc, false);
+                }
                 acc >>= a.hshift;
-                ring[((next_src + r) & mask) * TW + col] = static_cast<int16_t>(acc < 32767 ? acc : 32767);
+                const int R = (next_src + r) & mask;
+                // element ((R >> 1) * TW + col) * 2 + (R & 1), TW = 1 << twl
+                ring[(((R & ~1) << twl) | (R & 1)) + 2 * col] = static_cast<int16_t>(acc < 32767 ? acc : 32767);
                 s += r_step * S;
             }
         }
@@ -263,18 +300,23 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
             if (TW == kTileW) yy = __builtin_amdgcn_readfirstlane(yy);
             if (yy >= ny) break;
             const int y = y0 + yy;
-            const int vp = vpl[yy];
-            const int16_t *vc = vcl + yy * vt;
+            // byte offset of row pair vbase/2 in the ring; advancing one pair is
+            // + 4 * TW bytes, wrapped by the (power-of-two) ring size
+            int ro = (vpl[yy] & mask) << (J.twl + 1);
+            const int32_t *vc = vcl + yy * vtp;
             if (cx >= nx) continue;
             int acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
-#pragma unroll 4
-            for (int k = 0; k < vt; ++k) {
-                const int cf = vc[k];
-                const uint2 q = *reinterpret_cast<const uint2 *>(ring + ((vp + k) & mask) * TW + cx);
-                acc0 += static_cast<int>(static_cast<int16_t>(q.x & 0xffff)) * cf;
-                acc1 += static_cast<int>(static_cast<int16_t>(q.x >> 16)) * cf;
-                acc2 += static_cast<int>(static_cast<int16_t>(q.y & 0xffff)) * cf;
-                acc3 += static_cast<int>(static_cast<int16_t>(q.y >> 16)) * cf;
+            const uint8_t *rbase = reinterpret_cast<const uint8_t *>(ring) + cx * 4;
+#pragma unroll 2
+            for (int j = 0; j < vtp; ++j) {
+                const v2i16 cf = __builtin_bit_cast(v2i16, vc[j]);
+                // rows (2(pb+j), 2(pb+j)+1) of columns cx..cx+3: one 16-B read
+                const uint4 q = *reinterpret_cast<const uint4 *>(rbase + ro);
+                ro = (ro + (4 << J.twl)) & rbytes_mask;
+                acc0 = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.x), cf, acc0, false);
+                acc1 = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.y), cf, acc1, false);
+                acc2 = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.z), cf, acc2, false);
+                acc3 = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.w), cf, acc3, false);
             }
             const int x = x0 + cx;
             int o[4];
@@ -418,8 +460,38 @@ using pp::FilterBank;
 struct HostPlane {
     FilterBank::Compact h, v;
     std::vector<int32_t> c0, cn, lo, hi;
+    std::vector<int32_t> vbase, vcoef2;  // V window as even-aligned row pairs
+    int vtp = 1;
     int tiles_x = 0, nseg = 0, tw = 0, seg_h = 0, cho = 0, ring = 0, maxnew = 0, S = 0;
 };
+
+// Vertical taps regrouped as row pairs starting at an even row (the ring keeps
+// row pairs interleaved, so one 32-bit LDS word is a v_dot2 operand).  An odd
+// window start gets a leading zero tap; trailing zeros are dropped.
+void pair_rows(HostPlane &hp) {
+    const auto &v = hp.v;
+    const int n = (int)v.pos.size();
+    int vtp = 1;
+    for (int i = 0; i < n; ++i) {
+        int last = 0;
+        for (int k = 0; k < v.taps; ++k)
+            if (v.coef[(size_t)i * v.taps + k]) last = k;
+        vtp = std::max(vtp, ((v.pos[i] & 1) + last + 2) / 2);
+    }
+    hp.vtp = vtp;
+    hp.vbase.assign(n, 0);
+    hp.vcoef2.assign((size_t)n * vtp, 0);
+    for (int i = 0; i < n; ++i) {
+        const int odd = v.pos[i] & 1;
+        hp.vbase[i] = v.pos[i] - odd;
+        auto tap = [&](int k) -> uint16_t {
+            return (k >= 0 && k < v.taps) ? (uint16_t)v.coef[(size_t)i * v.taps + k] : 0;
+        };
+        for (int j = 0; j < vtp; ++j)
+            hp.vcoef2[(size_t)i * vtp + j] =
+                (int32_t)((uint32_t)tap(2 * j - odd) | ((uint32_t)tap(2 * j + 1 - odd) << 16));
+    }
+}
 
 // Column window of every strip for a strip width.
 int col_windows(HostPlane &hp, int sw, int dw, int tw) {
@@ -469,7 +541,7 @@ void row_chunks(HostPlane &hp, int sh, int dh, int cho, int seg_h, int *maxnew, 
             next = std::max(next, hp.hi[ci]);
         }
     }
-    int r = 1;
+    int r = 2;  // row pairs: at least one pair
     while (r < span) r <<= 1;
     *maxnew = std::max(mn, 1);
     *ring = r;
@@ -491,7 +563,7 @@ int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::
             int maxnew, ring;
             row_chunks(hp, sh, dh, cho, seg_h, &maxnew, &ring);
             const size_t bytes = (size_t)maxnew * S * 2 + (size_t)ring * tw * 2 +
-                                 (size_t)((cho * hp.v.taps + 1) & ~1) * 2 + (size_t)cho * 4;
+                                 (size_t)cho * hp.vtp * 4 + (size_t)cho * 4;
             if (bytes > (size_t)pp::kLdsBudget) continue;
             hp.tiles_x = (dw + tw - 1) / tw;
             hp.nseg = nseg; hp.tw = tw; hp.seg_h = seg_h; hp.cho = cho;
@@ -569,6 +641,7 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
         const int dst_w = c ? P->cdw : dw, dst_h = c ? P->cdh : dh;
         if (hp[c].h.taps != ht && P->f[c].compact(src_w, ht, &hp[c].h, &err))
             PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
+        pair_rows(hp[c]);
         if (plan_tiles(hp[c], src_w, src_h, dst_w, dst_h, &P->lds_bytes, &err))
             PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
     }
@@ -582,14 +655,14 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
     auto sz2 = [](size_t n) { return (n * 2 + 255) & ~size_t(255); };
     size_t total = 0;
     for (int c = 0; c < 2; ++c)
-        total += sz4(hp[c].h.pos.size()) + sz2(hp[c].h.coef.size()) + sz4(hp[c].v.pos.size()) +
-                 sz2(hp[c].v.coef.size()) + 2 * sz4(hp[c].c0.size()) + 2 * sz4(hp[c].lo.size());
+        total += sz4(hp[c].h.pos.size()) + sz2(hp[c].h.coef.size()) + sz4(hp[c].vbase.size()) +
+                 sz4(hp[c].vcoef2.size()) + 2 * sz4(hp[c].c0.size()) + 2 * sz4(hp[c].lo.size());
     PP_HIP(hipSetDevice(ctx->device));
     PP_HIP(hipMalloc(&P->dev, total));
     std::vector<uint8_t> host(total, 0);
     size_t off = 0;
-    const int32_t *dptr32[2][6];
-    const int16_t *dptr16[2][2];
+    const int32_t *dptr32[2][7];
+    const int16_t *dptr16[2][1];
     auto put = [&](const void *src, size_t bytes, size_t padded) {
         std::memcpy(host.data() + off, src, bytes);
         const void *d = static_cast<uint8_t *>(P->dev) + off;
@@ -599,8 +672,8 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
     for (int c = 0; c < 2; ++c) {
         dptr32[c][0] = (const int32_t *)put(hp[c].h.pos.data(), hp[c].h.pos.size() * 4, sz4(hp[c].h.pos.size()));
         dptr16[c][0] = (const int16_t *)put(hp[c].h.coef.data(), hp[c].h.coef.size() * 2, sz2(hp[c].h.coef.size()));
-        dptr32[c][1] = (const int32_t *)put(hp[c].v.pos.data(), hp[c].v.pos.size() * 4, sz4(hp[c].v.pos.size()));
-        dptr16[c][1] = (const int16_t *)put(hp[c].v.coef.data(), hp[c].v.coef.size() * 2, sz2(hp[c].v.coef.size()));
+        dptr32[c][1] = (const int32_t *)put(hp[c].vbase.data(), hp[c].vbase.size() * 4, sz4(hp[c].vbase.size()));
+        dptr32[c][6] = (const int32_t *)put(hp[c].vcoef2.data(), hp[c].vcoef2.size() * 4, sz4(hp[c].vcoef2.size()));
         dptr32[c][2] = (const int32_t *)put(hp[c].c0.data(), hp[c].c0.size() * 4, sz4(hp[c].c0.size()));
         dptr32[c][3] = (const int32_t *)put(hp[c].cn.data(), hp[c].cn.size() * 4, sz4(hp[c].cn.size()));
         dptr32[c][4] = (const int32_t *)put(hp[c].lo.data(), hp[c].lo.size() * 4, sz4(hp[c].lo.size()));
@@ -615,13 +688,15 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
         J.sw = c ? P->csw : sw; J.sh = c ? P->csh : sh;
         J.dw = c ? P->cdw : dw; J.dh = c ? P->cdh : dh;
         J.tiles_x = hp[c].tiles_x; J.tiles_y = hp[c].nseg; J.tw = hp[c].tw;
+        J.twl = 0;
+        while ((1 << J.twl) < J.tw) ++J.twl;
         J.seg_h = hp[c].seg_h; J.cho = hp[c].cho;
         J.tile_base = base;
         base += J.tiles_x * J.tiles_y;
-        J.vt = hp[c].v.taps; J.ring = hp[c].ring; J.maxnew = hp[c].maxnew; J.S = hp[c].S;
+        J.vtp = hp[c].vtp; J.ring = hp[c].ring; J.maxnew = hp[c].maxnew; J.S = hp[c].S;
         J.dither_off = p == 2 ? 3 : 0;
         J.hpos = dptr32[c][0]; J.hcoef = dptr16[c][0];
-        J.vpos = dptr32[c][1]; J.vcoef = dptr16[c][1];
+        J.vbase = dptr32[c][1]; J.vcoef2 = dptr32[c][6];
         J.tile_c0 = dptr32[c][2]; J.tile_cn = dptr32[c][3];
         J.chunk_lo = dptr32[c][4]; J.chunk_hi = dptr32[c][5];
     }

@@ -7,7 +7,7 @@
 //   SI_n = std over rows 1..H-2, cols 1..W-2 of sqrt(Gx^2 + Gy^2)  (Sobel 3x3)
 //   TI_n = std over the full frame of Y_n - Y_{n-1}                (n >= 1)
 //
-// Layout: a workgroup (256 lanes) owns a 2048-px x 16-row band of the frame
+// Layout: a workgroup (256 lanes, 4 waves) owns a 2048-px x 16-row band of the frame
 // and walks a contiguous chunk of frames.  Each lane holds 8 adjacent pixels
 // of a row (one 16-B or 8-B load), gets its left/right neighbours by lane
 // shuffles (global loads only at wave edges), and slides a 3-row window down
@@ -24,6 +24,7 @@
 // sum(d^2) exact in 64-bit integers.  Per (frame, band) partials are written
 // without atomics and reduced in a fixed order by siti_finalize, so results
 // are bit-reproducible.
+#include <algorithm>
 #include <cmath>
 
 #include "common.hpp"
@@ -32,7 +33,8 @@ namespace pp {
 
 constexpr int kBand = 16;
 constexpr int kLanePx = 8;
-constexpr int kSpan = 256 * kLanePx;  // 2048 px per workgroup
+constexpr int kWaveSpan = 62 * kLanePx;  // 496 px per wave: lanes 0 and 63 are halo lanes
+constexpr int kSpan = 4 * kWaveSpan;     // 1984 px per workgroup
 
 struct SitiPartial {
     double mean;   // mean of |G| over n samples
@@ -76,6 +78,8 @@ __device__ inline void load_row(int v[kLanePx], const T *row, int x, int W, bool
     }
 }
 
+constexpr int kOob = 0x7ffffff0;  // buffer offset past any num_records: reads 0, no memory access
+
 __device__ inline uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -92,61 +96,121 @@ __device__ inline void chan_merge_f(float &n, float &mean, float &m2, float nb, 
     n = nn;
 }
 
+// One row of a lane's 8 pixels in load format: 4 dwords (u16) or 2 (u8).
 template <typename T>
-__device__ inline void pack_row(uint32_t pk[4], const int v[kLanePx]) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) pk[e] = (uint32_t)v[2 * e] | ((uint32_t)v[2 * e + 1] << 16);
+struct Row {
+    static constexpr int N = sizeof(T) == 2 ? 4 : 2;
+    uint32_t w[N];
+    __device__ int px(int e) const {
+        if constexpr (sizeof(T) == 2) return (w[e >> 1] >> (16 * (e & 1))) & 0xffff;
+        else return (w[e >> 2] >> (8 * (e & 3))) & 0xff;
+    }
+};
+
+// Issue the load of one row (bounds-checked buffer load; kOob reads 0).
+template <typename T>
+__device__ inline void issue_row(Row<T> &r, __amdgpu_buffer_rsrc_t rs, int off) {
+    if constexpr (sizeof(T) == 2) {
+        const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        __builtin_memcpy(r.w, &q, 16);
+    } else {
+        const auto q = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+        __builtin_memcpy(r.w, &q, 8);
+    }
 }
 
+// Unaligned fallback: element loads, zero outside [0, W) and outside the frame.
 template <typename T>
+__device__ inline void load_row_slow(Row<T> &r, const uint8_t *frame, int64_t ls, int row, int H, int x, int W) {
+    int v[kLanePx] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (frame && row >= 0 && row < H) load_row<T>(v, reinterpret_cast<const T *>(frame + (int64_t)row * ls), x, W, false);
+#pragma unroll
+    for (int i = 0; i < Row<T>::N; ++i) r.w[i] = 0;
+#pragma unroll
+    for (int e = 0; e < kLanePx; ++e) {
+        if constexpr (sizeof(T) == 2) r.w[e >> 1] |= (uint32_t)v[e] << (16 * (e & 1));
+        else r.w[e >> 2] |= (uint32_t)v[e] << (8 * (e & 3));
+    }
+}
+
+// Window of a workgroup's band: rows y0-1 .. y0+kBand of one frame, held as
+// raw load registers.  Row ri's registers are reloaded with the NEXT frame's
+// row ri right after frame f consumes them, so a whole frame of loads is in
+// flight while the current one is computed, with no extra registers and no
+// branches around the loads.  The previous frame's band (TI) stays in
+// registers too, so every pixel is read from HBM once (plus the two halo rows).
+template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_t ls, int64_t fs, int nframes,
                                                    const uint8_t *prev, int W, int H, int tiles_x, int bands,
-                                                   int chunk, int vec, SitiPartial *part) {
-    __shared__ SitiPartial red[4];
+                                                   int chunk, SitiPartial *part) {
+    constexpr int NR = kBand + 2;
     const int tile = blockIdx.x;  // tx + tiles_x * band
     const int tx = tile % tiles_x, band = tile / tiles_x;
     const int f0 = blockIdx.y * chunk, f1 = min(nframes, f0 + chunk);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = tx * kSpan + threadIdx.x * kLanePx;
+    // lanes 1..62 own 8 pixels each; lanes 0 and 63 load the pixels just left
+    // and right of the wave's span, so every neighbour comes from a shuffle
+    const int x = tx * kSpan + wave * kWaveSpan + (lane - 1) * kLanePx;
+    const bool halo = lane == 0 || lane == 63;
     const int y0 = band * kBand, y1 = min(H, y0 + kBand);
-    const bool wave_left = lane == 0, wave_right = lane == 63;
-    int valid_px = 0;  // pixels of this lane inside the frame
+    int valid_px = 0;  // pixels this lane accounts for (TI)
 #pragma unroll
-    for (int e = 0; e < kLanePx; ++e) valid_px += (x + e < W);
-    int sobel_lo = 1 - x, sobel_hi = W - 2 - x;  // lane-relative valid Sobel columns [lo, hi]
+    for (int e = 0; e < kLanePx; ++e) valid_px += (!halo && x + e >= 0 && x + e < W);
+    // lane-relative valid Sobel columns [lo, hi] (empty for halo lanes)
+    const int sobel_lo = halo ? kLanePx : 1 - x, sobel_hi = halo ? -1 : W - 2 - x;
 
-    // previous frame's band, packed 2 samples per register (TI without re-reading HBM)
-    uint32_t pv[kBand][4];
+    const int frame_bytes = (int)((int64_t)(H - 1) * ls + (int64_t)W * sizeof(T));
+    const int xb = x * (int)sizeof(T);
+    const bool x_in = x >= 0 && x < W;  // lane 0 of the first wave sits left of the frame
+    auto rsrc = [&](const uint8_t *base) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), (short)0, frame_bytes, 0x00020000);
+    };
+    auto row_off = [&](int r, bool live) { return (live && x_in && r >= 0 && r < H) ? r * (int)ls + xb : kOob; };
+
+    Row<T> raw[NR], pv[kBand];
+    // previous frame's band
     const uint8_t *pfirst = f0 > 0 ? frames + (f0 - 1) * fs : prev;
-    if (pfirst) {
+    const bool have_pfirst = pfirst != nullptr && f0 < f1;
+    {
+        const auto prs = rsrc(have_pfirst ? pfirst : frames);
 #pragma unroll
         for (int i = 0; i < kBand; ++i) {
-            int q[kLanePx] = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (y0 + i < y1) load_row<T>(q, reinterpret_cast<const T *>(pfirst + (int64_t)(y0 + i) * ls), x, W, vec);
-            pack_row<T>(pv[i], q);
+            if constexpr (VEC) issue_row<T>(pv[i], prs, row_off(y0 + i, have_pfirst && y0 + i < y1));
+            else load_row_slow<T>(pv[i], have_pfirst && x_in && y0 + i < y1 ? pfirst : nullptr, ls, y0 + i, H, x, W);
+        }
+    }
+    // first frame's window
+    {
+        const uint8_t *fb = frames + (int64_t)f0 * fs;
+        const bool live = f0 < f1;
+        const auto crs = rsrc(live ? fb : frames);
+#pragma unroll
+        for (int ri = 0; ri < NR; ++ri) {
+            const int r = y0 - 1 + ri;
+            if constexpr (VEC) issue_row<T>(raw[ri], crs, row_off(r, live));
+            else load_row_slow<T>(raw[ri], live && x_in ? fb : nullptr, ls, r, H, x, W);
         }
     }
 
     for (int f = f0; f < f1; ++f) {
-        const uint8_t *cur = frames + f * fs;
         const bool has_prev = f > 0 || prev != nullptr;
+        const bool nlive = f + 1 < f1;
+        const uint8_t *nb = frames + (int64_t)(nlive ? f + 1 : f) * fs;
+        const auto nrs = rsrc(nb);
         float n_t = 0.f, mean_t = 0.f, m2_t = 0.f;
         uint64_t d2s = 0;
         int64_t d1s = 0;
         int h1a[kLanePx], h2a[kLanePx], h1b[kLanePx], h2b[kLanePx];
-        // rows y0-1 .. y0+kBand, fully unrolled so the band index is a constant
 #pragma unroll
-        for (int ri = 0; ri < kBand + 2; ++ri) {
+        for (int ri = 0; ri < NR; ++ri) {
             const int r = y0 - 1 + ri;
-            int v[kLanePx] = {0, 0, 0, 0, 0, 0, 0, 0};
+            int v[kLanePx];
+#pragma unroll
+            for (int e = 0; e < kLanePx; ++e) v[e] = raw[ri].px(e);
             int h1[kLanePx], h2[kLanePx];
-            if (r >= 0 && r < H) {
-                const T *row = reinterpret_cast<const T *>(cur + (int64_t)r * ls);
-                load_row<T>(v, row, x, W, vec);
-                int left = __shfl_up(v[kLanePx - 1], 1, 64);
-                int right = __shfl_down(v[0], 1, 64);
-                if (wave_left) left = (x - 1 >= 0 && x - 1 < W) ? static_cast<int>(row[x - 1]) : 0;
-                if (wave_right) right = (x + kLanePx < W) ? static_cast<int>(row[x + kLanePx]) : 0;
+            {
+                const int left = __shfl_up(v[kLanePx - 1], 1, 64);   // garbage only on halo lanes
+                const int right = __shfl_down(v[0], 1, 64);
 #pragma unroll
                 for (int e = 0; e < kLanePx; ++e) {
                     const int l = e ? v[e - 1] : left;
@@ -154,27 +218,23 @@ __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_
                     h1[e] = rr - l;
                     h2[e] = l + 2 * v[e] + rr;
                 }
-            } else {
-#pragma unroll
-                for (int e = 0; e < kLanePx; ++e) h1[e] = h2[e] = 0;
             }
-            // TI on the band rows, previous frame from registers
+            // TI on the band rows against the previous frame's band
             const int bi = ri - 1;
-            if (ri >= 1 && ri <= kBand && r < y1) {
-                if (has_prev) {
+            if (ri >= 1 && ri <= kBand) {
+                if (has_prev && r < y1) {
                     int ds = 0;
                     uint32_t dq = 0;
 #pragma unroll
                     for (int e = 0; e < kLanePx; ++e) {
-                        const int q = (pv[bi][e >> 1] >> (16 * (e & 1))) & 0xffff;
-                        const int d = (e < valid_px) ? v[e] - q : 0;
+                        const int d = (e < valid_px) ? v[e] - pv[bi].px(e) : 0;
                         ds += d;
                         dq += static_cast<uint32_t>(d * d);
                     }
                     d1s += ds;
                     d2s += dq;
                 }
-                pack_row<T>(pv[bi], v);
+                pv[bi] = raw[ri];
             }
             // Sobel centred on row c = r - 1 (rows c-1, c, c+1 are in the window)
             const int c = r - 1;
@@ -207,57 +267,66 @@ __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_
                 h1a[e] = h1b[e]; h2a[e] = h2b[e];
                 h1b[e] = h1[e]; h2b[e] = h2[e];
             }
+            // this row is consumed: start loading the next frame's row ri into it
+            if constexpr (VEC) issue_row<T>(raw[ri], nrs, row_off(r, nlive));
+            else load_row_slow<T>(raw[ri], nlive && x_in ? nb : nullptr, ls, r, H, x, W);
         }
-        // block reduction (fixed order, fp64) -> one partial per (frame, tile)
+        // wave reduction (fixed order, fp64) -> one partial per (frame, tile, wave)
         int64_t cnt = static_cast<int64_t>(n_t);
         double mean = mean_t, m2 = m2_t;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
-            const int64_t nb = __shfl_xor(cnt, o, 64);
+            const int64_t nb2 = __shfl_xor(cnt, o, 64);
             const double mb = __shfl_xor(mean, o, 64), qb = __shfl_xor(m2, o, 64);
             // both lanes of a pair merge (lower, upper) in the same order
-            if ((lane & o) == 0) chan_merge(cnt, mean, m2, nb, mb, qb);
+            if ((lane & o) == 0) chan_merge(cnt, mean, m2, nb2, mb, qb);
             else {
-                int64_t n2 = nb; double mm = mb, qq = qb;
+                int64_t n2 = nb2; double mm = mb, qq = qb;
                 chan_merge(n2, mm, qq, cnt, mean, m2);
                 cnt = n2; mean = mm; m2 = qq;
             }
         }
         d1s = static_cast<int64_t>(wave_sum_u64(static_cast<uint64_t>(d1s)));
         d2s = wave_sum_u64(d2s);
-        if (lane == 0) red[wave] = {mean, m2, cnt, d1s, d2s, 0};
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            SitiPartial o = red[0];
-            for (int w = 1; w < 4; ++w) {
-                chan_merge(o.n, o.mean, o.m2, red[w].n, red[w].mean, red[w].m2);
-                o.d1 += red[w].d1; o.d2 += red[w].d2;
-            }
-            part[(int64_t)f * tiles_x * bands + tile] = o;
-        }
-        __syncthreads();
+        if (lane == 0) part[((int64_t)f * tiles_x * bands + tile) * 4 + wave] = {mean, m2, cnt, d1s, d2s, 0};
     }
 }
 
-__global__ void siti_finalize(const SitiPartial *part, int nframes, int ntiles, int W, int H, int has_prev,
-                              double *si, double *ti) {
-    const int f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= nframes) return;
+// One workgroup per frame: each lane merges a strided subset of the partials,
+// then a fixed-shape LDS tree -- the order never depends on timing, so the
+// result is bit-reproducible.
+__global__ __launch_bounds__(256) void siti_finalize(const SitiPartial *part, int nframes, int nparts, int W, int H,
+                                                     int has_prev, double *si, double *ti) {
+    __shared__ double s_mean[256], s_m2[256];
+    __shared__ int64_t s_n[256], s_d1[256];
+    __shared__ uint64_t s_d2[256];
+    const int f = blockIdx.x, t = threadIdx.x;
     double mean = 0.0, m2 = 0.0;
     int64_t n = 0, d1 = 0;
     uint64_t d2 = 0;
-    for (int t = 0; t < ntiles; ++t) {
-        const SitiPartial &p = part[(int64_t)f * ntiles + t];
+    for (int i = t; i < nparts; i += 256) {
+        const SitiPartial &p = part[(int64_t)f * nparts + i];
         chan_merge(n, mean, m2, p.n, p.mean, p.m2);
         d1 += p.d1; d2 += p.d2;
     }
-    si[f] = n ? sqrt(m2 / static_cast<double>(n)) : 0.0;
+    s_mean[t] = mean; s_m2[t] = m2; s_n[t] = n; s_d1[t] = d1; s_d2[t] = d2;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) {
+            chan_merge(s_n[t], s_mean[t], s_m2[t], s_n[t + o], s_mean[t + o], s_m2[t + o]);
+            s_d1[t] += s_d1[t + o];
+            s_d2[t] += s_d2[t + o];
+        }
+        __syncthreads();
+    }
+    if (t) return;
+    si[f] = s_n[0] ? sqrt(s_m2[0] / static_cast<double>(s_n[0])) : 0.0;
     if (f == 0 && !has_prev) {
         ti[f] = __builtin_nan("");
     } else {
         const int64_t np = static_cast<int64_t>(W) * H;
-        const __int128 num = static_cast<__int128>(np) * static_cast<__int128>(d2) -
-                             static_cast<__int128>(d1) * static_cast<__int128>(d1);
+        const __int128 num = static_cast<__int128>(np) * static_cast<__int128>(s_d2[0]) -
+                             static_cast<__int128>(s_d1[0]) * static_cast<__int128>(s_d1[0]);
         ti[f] = sqrt(static_cast<double>(num)) / static_cast<double>(np);
     }
 }
@@ -277,27 +346,32 @@ extern "C" int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma
     const int bytes = bitdepth > 8 ? 2 : 1;
     const int tiles_x = (w + kSpan - 1) / kSpan, bands = (h + kBand - 1) / kBand;
     const int ntiles = tiles_x * bands;
-    // ~4 workgroups per CU, frames chunked per workgroup (each chunk re-reads one
-    // previous frame band for TI, so chunks stay long)
-    int chunks = (1024 + ntiles - 1) / ntiles;
+    // frames chunked per workgroup so that the grid is one wave of resident
+    // workgroups (a partial second wave would idle most of the chip); each chunk
+    // re-reads one previous-frame band for TI, so chunks stay long
+    int dev_cus = 0, per_cu = 0;
+    PP_HIP(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    PP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, bytes == 2 ? (const void *)siti_kernel<uint16_t, true> : (const void *)siti_kernel<uint8_t, true>, 256, 0));
+    const int slots = std::max(1, dev_cus * std::max(1, per_cu));
+    int chunks = std::max(1, slots / ntiles);
     if (chunks > nframes) chunks = nframes;
     if (chunks > 65535) chunks = 65535;
     const int chunk = (nframes + chunks - 1) / chunks;
     chunks = (nframes + chunk - 1) / chunk;
     const int a = bytes == 2 ? 16 : 8;
     const int vec = ((uintptr_t)luma % a == 0) && (linesize % a == 0) && (nframes < 2 || frame_stride % a == 0) &&
-                    (!prev || (uintptr_t)prev % a == 0);
+                    (!prev || (uintptr_t)prev % a == 0) &&
+                    ((int64_t)(h - 1) * linesize + (int64_t)w * bytes < (int64_t)kOob);
     SitiPartial *part = nullptr;
-    PP_HIP(hipMallocAsync((void **)&part, sizeof(SitiPartial) * (size_t)ntiles * nframes, st));
+    PP_HIP(hipMallocAsync((void **)&part, sizeof(SitiPartial) * (size_t)ntiles * 4 * nframes, st));
     dim3 grid(ntiles, chunks);
-    if (bytes == 2)
-        hipLaunchKernelGGL(siti_kernel<uint16_t>, grid, dim3(256), 0, st, (const uint8_t *)luma, linesize,
-                           frame_stride, nframes, (const uint8_t *)prev, w, h, tiles_x, bands, chunk, vec, part);
-    else
-        hipLaunchKernelGGL(siti_kernel<uint8_t>, grid, dim3(256), 0, st, (const uint8_t *)luma, linesize,
-                           frame_stride, nframes, (const uint8_t *)prev, w, h, tiles_x, bands, chunk, vec, part);
-    hipLaunchKernelGGL(siti_finalize, dim3((nframes + 255) / 256), dim3(256), 0, st, part, nframes, ntiles, w, h,
-                       prev != nullptr, si, ti);
+    auto k = bytes == 2 ? (vec ? siti_kernel<uint16_t, true> : siti_kernel<uint16_t, false>)
+                        : (vec ? siti_kernel<uint8_t, true> : siti_kernel<uint8_t, false>);
+    hipLaunchKernelGGL(k, grid, dim3(256), 0, st, (const uint8_t *)luma, linesize, frame_stride, nframes,
+                       (const uint8_t *)prev, w, h, tiles_x, bands, chunk, part);
+    hipLaunchKernelGGL(siti_finalize, dim3(nframes), dim3(256), 0, st, part, nframes, ntiles * 4, w, h,
+                       prev != nullptr, si, ti);  // ntiles * 4 wave partials per frame
     PP_HIP(hipGetLastError());
     PP_HIP(hipFreeAsync(part, st));
     return PP_OK;

@@ -83,3 +83,35 @@ def test_siti_config2_length(gpu):
         rti = siti_ref.ti_frame(frames[i], frames[i - 1])
         assert abs(si[i] - rsi) <= RTOL_SI * abs(rsi)
         assert abs(ti[i] - rti) <= 1e-12 * max(1.0, abs(rti))
+
+
+@pytest.mark.parametrize("depth,w", [(10, 1984), (10, 1985), (8, 497), (8, 496), (10, 3969)])
+def test_siti_tile_and_wave_boundaries(gpu, depth, w):
+    """Widths around the 496-px wave span and the 1984-px workgroup span."""
+    fmt = po.YUV420P10LE if depth > 8 else po.YUV420P
+    rng = np.random.default_rng(w)
+    frames = np.stack([synth.noise_frame(rng, fmt, w, 37)[0] for _ in range(3)])
+    si, ti = _run(frames, depth, gpu)
+    rsi, rti = siti_ref.siti(frames)
+    np.testing.assert_allclose(si, rsi, rtol=RTOL_SI, atol=1e-9)
+    np.testing.assert_allclose(ti[1:], rti[1:], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("depth", [8, 10])
+def test_siti_unaligned_pitched_view(gpu, depth):
+    """A pitched view starting one sample into each row takes the unaligned path."""
+    import torch
+    from pixpath import ops
+    fmt = po.YUV420P10LE if depth > 8 else po.YUV420P
+    rng = np.random.default_rng(5)
+    w, h, n = 643, 41, 5
+    frames = np.stack([synth.noise_frame(rng, fmt, w, h)[0] for _ in range(n)])
+    dt = np.uint16 if depth > 8 else np.uint8
+    big = np.zeros((n, h, w + 5), dt)
+    big[:, :, 1:w + 1] = frames
+    t = torch.from_numpy(big).to(gpu)[:, :, 1:w + 1]
+    si, ti = ops.siti(t, depth)
+    torch.cuda.synchronize()
+    rsi, rti = siti_ref.siti(frames)
+    np.testing.assert_allclose(si.cpu().numpy(), rsi, rtol=RTOL_SI, atol=1e-9)
+    np.testing.assert_allclose(ti.cpu().numpy()[1:], rti[1:], rtol=1e-12, atol=1e-12)

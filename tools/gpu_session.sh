@@ -4,9 +4,13 @@ set -o pipefail
 TAG=${1:-run}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu_$TAG.log 2>&1; echo "pytest rc=$?"
-grep -E "passed|failed" gpurun_out/pytest_gpu_$TAG.log | tail -3
-grep -E "^FAILED" gpurun_out/pytest_gpu_$TAG.log | head -20
+TESTS=${TESTS:-tests}
+timeout -k 10 600 python -m pytest $TESTS -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?
+echo "pytest rc=$rc"
+tail -3 gpurun_out/pytest_gpu_$TAG.log
+grep -E "^FAILED" gpurun_out/pytest_gpu_$TAG.log | head -20 || true
+# 0 = green, 1 = test failures: keep going; anything else (crash, abort, timeout) ends the call
+if [ $rc -gt 1 ]; then echo "stopping after pytest rc=$rc"; exit $rc; fi
 timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err && cat gpurun_out/bench_$TAG.json &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt_$TAG -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof_kt_$TAG.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch_$TAG -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > gpurun_out/prof_fetch_$TAG.log 2>&1 &&
