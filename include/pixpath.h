@@ -55,7 +55,10 @@ enum pp_pix_fmt {
 /*
  * A batch of `nframes` frames.  Plane p of frame f starts at
  * data[p] + f * frame_stride[p]; rows are linesize[p] bytes apart.
- * Packed formats use plane 0 only.
+ * Packed formats use plane 0 only.  Every row of a plane, the last one
+ * included, must be readable for min(linesize, width rounded up to 16 bytes)
+ * bytes: with 16-byte aligned pointers and linesizes the kernels read whole
+ * 16-byte granules (a plane allocated as height x linesize always qualifies).
  */
 typedef struct pp_frames {
     void *data[3];

@@ -54,6 +54,19 @@ inline FmtInfo fmt_info(int f) {
 
 inline int ceil_rshift(int a, int s) { return -((-a) >> s); }
 
+// MI355X dispatches the workgroups of a 1-D grid round-robin over its 8 XCDs
+// (block b -> XCD b % 8), each with its own L2.  Remapping hardware block `b`
+// to logical work item `xcd_remap(b, n)` gives XCD k the contiguous range
+// [k*n/8, (k+1)*n/8) in order, so neighbouring work items (strips of one
+// frame, bands of one frame range) share an L2 and their halos are fetched
+// from HBM once.  A bijection on [0, n) for any n.
+constexpr int kXcds = 8;
+__host__ __device__ inline int xcd_remap(int b, int n) {
+    const int per = n / kXcds, rem = n % kXcds;
+    const int k = b % kXcds, q = b / kXcds;
+    return k < rem ? k * (per + 1) + q : rem * (per + 1) + (k - rem) * per + q;
+}
+
 struct Ctx {
     int device = 0;
     // spinner animation (PP-STALL-1), device resident

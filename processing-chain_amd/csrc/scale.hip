@@ -26,6 +26,7 @@
 #include <memory>
 
 #include "common.hpp"
+#include "device.hpp"
 #include "filters.hpp"
 
 namespace pp {
@@ -62,6 +63,7 @@ struct ScaleArgs {
     uint8_t *dst[3];
     int64_t dls[3], dfs[3];
     int nplanes;
+    int tiles;    // workgroups per frame (all planes)
     int hshift;   // 7 for 8-bit sources, depth-1 otherwise
     int dither;   // ordered dither (>8-bit source narrowed to 8 bit)
     int vec_src;  // all source rows 16-B aligned
@@ -101,7 +103,6 @@ __device__ inline uint4 bload16(__amdgpu_buffer_rsrc_t rs, int off) {
     __builtin_memcpy(&r, &v, 16);
     return r;
 }
-constexpr int kOobOff = 0x7ffffff0;  // any offset >= num_records
 
 typedef int16_t v2i16 __attribute__((ext_vector_type(2)));
 
@@ -132,8 +133,11 @@ __device__ inline void store16(uint16_t *lds_dst, uint4 v) {
 template <typename ST, int OUTB, int HT>
 __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     extern __shared__ __align__(16) uint16_t lds[];
-    const int frame = blockIdx.y;
-    int t = blockIdx.x;
+    // 1-D grid of frames x tiles, XCD-aware: an XCD walks consecutive strips of
+    // consecutive frames, so strip and segment halos hit its L2
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int frame = L / a.tiles;
+    int t = L - frame * a.tiles;
     int p = 0;
     if (a.nplanes > 1 && t >= a.pl[1].tile_base) p = 1;
     if (a.nplanes > 2 && t >= a.pl[2].tile_base) p = 2;
@@ -193,8 +197,11 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     const int64_t sls = a.sls[p];
     const bool vec = a.vec_src;
     const int sw = J.sw;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<ST *>(sbase), (short)0, (int)((int64_t)(J.sh - 1) * sls + (int64_t)sw * sizeof(ST)), 0x00020000);
+    // a 16-B load that straddles num_records reads 0 as a whole, so the last
+    // row counts up to its 16-B-rounded width (inside the pitch: the vector
+    // path requires 16-B aligned linesizes; see pp_frames in pixpath.h)
+    const int64_t last_row = std::min<int64_t>(sls, ((int64_t)sw * sizeof(ST) + 15) & ~int64_t(15));
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(sbase, (int)((int64_t)(J.sh - 1) * sls + last_row));
     const int cbyte = c0 * (int)sizeof(ST);
     // byte offset of chunk `id` of rows [from, ...) (kOobOff when id >= total)
     auto chunk_off = [&](int id, int from, int total) {
@@ -757,14 +764,16 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
         k = out_depth == 8 ? pick_ht<uint16_t, 8>(P->ht) : pick_ht<uint16_t, 10>(P->ht);
     if (!k) PP_FAIL(PP_ERR_UNSUPPORTED, "no kernel for %d taps", P->ht);
     const int tiles = P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y;
-    for (int f0 = 0; f0 < nframes; f0 += 65535) {
-        const int nf = std::min(65535, nframes - f0);
+    a.tiles = tiles;
+    const int fmax = std::max(1, (1 << 30) / tiles);  // 1-D grid size limit
+    for (int f0 = 0; f0 < nframes; f0 += fmax) {
+        const int nf = std::min(fmax, nframes - f0);
         ScaleArgs b = a;
         for (int p = 0; p < 3; ++p) {
             b.src[p] += f0 * a.sfs[p];
             b.dst[p] += f0 * a.dfs[p];
         }
-        hipLaunchKernelGGL(k, dim3(tiles, nf), dim3(kThreads), P->lds_bytes, st, b);
+        hipLaunchKernelGGL(k, dim3(tiles * nf), dim3(kThreads), P->lds_bytes, st, b);
     }
     PP_HIP(hipGetLastError());
     return PP_OK;

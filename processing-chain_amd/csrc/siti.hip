@@ -28,6 +28,7 @@
 #include <cmath>
 
 #include "common.hpp"
+#include "device.hpp"
 
 namespace pp {
 
@@ -78,7 +79,7 @@ __device__ inline void load_row(int v[kLanePx], const T *row, int x, int W, bool
     }
 }
 
-constexpr int kOob = 0x7ffffff0;  // buffer offset past any num_records: reads 0, no memory access
+constexpr int kOob = kOobOff;
 
 __device__ inline uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
@@ -144,9 +145,14 @@ __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_
                                                    const uint8_t *prev, int W, int H, int tiles_x, int bands,
                                                    int chunk, SitiPartial *part) {
     constexpr int NR = kBand + 2;
-    const int tile = blockIdx.x;  // tx + tiles_x * band
+    // 1-D grid of frame chunks x tiles, XCD-aware: an XCD holds consecutive
+    // bands of one frame chunk, so the halo rows shared by adjacent bands hit its L2
+    const int ntiles = tiles_x * bands;
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int ck = L / ntiles;
+    const int tile = L - ck * ntiles;  // tx + tiles_x * band
     const int tx = tile % tiles_x, band = tile / tiles_x;
-    const int f0 = blockIdx.y * chunk, f1 = min(nframes, f0 + chunk);
+    const int f0 = ck * chunk, f1 = min(nframes, f0 + chunk);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // lanes 1..62 own 8 pixels each; lanes 0 and 63 load the pixels just left
     // and right of the wave's span, so every neighbour comes from a shuffle
@@ -159,12 +165,13 @@ __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_
     // lane-relative valid Sobel columns [lo, hi] (empty for halo lanes)
     const int sobel_lo = halo ? kLanePx : 1 - x, sobel_hi = halo ? -1 : W - 2 - x;
 
-    const int frame_bytes = (int)((int64_t)(H - 1) * ls + (int64_t)W * sizeof(T));
+    // a row load straddling num_records reads 0 as a whole: the last row counts
+    // up to its load-granule-rounded width, which lies inside the (aligned) pitch
+    constexpr int G = kLanePx * sizeof(T);
+    const int frame_bytes = (int)((int64_t)(H - 1) * ls + min(ls, ((int64_t)W * sizeof(T) + G - 1) / G * G));
     const int xb = x * (int)sizeof(T);
     const bool x_in = x >= 0 && x < W;  // lane 0 of the first wave sits left of the frame
-    auto rsrc = [&](const uint8_t *base) {
-        return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), (short)0, frame_bytes, 0x00020000);
-    };
+    auto rsrc = [&](const uint8_t *base) { return uniform_rsrc(base, frame_bytes); };
     auto row_off = [&](int r, bool live) { return (live && x_in && r >= 0 && r < H) ? r * (int)ls + xb : kOob; };
 
     Row<T> raw[NR], pv[kBand];
@@ -356,7 +363,6 @@ extern "C" int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma
     const int slots = std::max(1, dev_cus * std::max(1, per_cu));
     int chunks = std::max(1, slots / ntiles);
     if (chunks > nframes) chunks = nframes;
-    if (chunks > 65535) chunks = 65535;
     const int chunk = (nframes + chunks - 1) / chunks;
     chunks = (nframes + chunk - 1) / chunk;
     const int a = bytes == 2 ? 16 : 8;
@@ -365,7 +371,7 @@ extern "C" int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma
                     ((int64_t)(h - 1) * linesize + (int64_t)w * bytes < (int64_t)kOob);
     SitiPartial *part = nullptr;
     PP_HIP(hipMallocAsync((void **)&part, sizeof(SitiPartial) * (size_t)ntiles * 4 * nframes, st));
-    dim3 grid(ntiles, chunks);
+    dim3 grid(ntiles * chunks);
     auto k = bytes == 2 ? (vec ? siti_kernel<uint16_t, true> : siti_kernel<uint16_t, false>)
                         : (vec ? siti_kernel<uint8_t, true> : siti_kernel<uint8_t, false>);
     hipLaunchKernelGGL(k, grid, dim3(256), 0, st, (const uint8_t *)luma, linesize, frame_stride, nframes,

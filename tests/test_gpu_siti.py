@@ -115,3 +115,24 @@ def test_siti_unaligned_pitched_view(gpu, depth):
     rsi, rti = siti_ref.siti(frames)
     np.testing.assert_allclose(si.cpu().numpy(), rsi, rtol=RTOL_SI, atol=1e-9)
     np.testing.assert_allclose(ti.cpu().numpy()[1:], rti[1:], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("depth,w", [(8, 333), (10, 1366)])
+def test_siti_padded_pitch(gpu, depth, w):
+    """Aligned pitched rows wider than the frame (vector path, partial last granule)."""
+    import torch
+    from pixpath import ops
+    fmt = po.YUV420P10LE if depth > 8 else po.YUV420P
+    rng = np.random.default_rng(w)
+    h, n = 45, 4
+    frames = np.stack([synth.noise_frame(rng, fmt, w, h)[0] for _ in range(n)])
+    dt = np.uint16 if depth > 8 else np.uint8
+    pitch = (w + 63) // 64 * 64
+    big = np.full((n, h, pitch), 7, dt)
+    big[:, :, :w] = frames
+    t = torch.from_numpy(big).to(gpu)[:, :, :w]
+    si, ti = ops.siti(t, depth)
+    torch.cuda.synchronize()
+    rsi, rti = siti_ref.siti(frames)
+    np.testing.assert_allclose(si.cpu().numpy(), rsi, rtol=RTOL_SI, atol=1e-9)
+    np.testing.assert_allclose(ti.cpu().numpy()[1:], rti[1:], rtol=1e-12, atol=1e-12)
