@@ -130,7 +130,10 @@ __device__ inline void store16(uint16_t *lds_dst, uint4 v) {
     }
 }
 
-template <typename ST, int OUTB, int HT>
+// TWC: 256 when every plane uses 256-column strips (the usual case: lane =
+// column, wave = row group, all row loops wave-uniform), 0 for the general
+// strip width.
+template <typename ST, int OUTB, int HT, int TWC>
 __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     extern __shared__ __align__(16) uint16_t lds[];
     // 1-D grid of frames x tiles, XCD-aware: an XCD walks consecutive strips of
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     const PlaneJob &J = a.pl[p];
     t -= J.tile_base;
     const int seg = t / J.tiles_x, tx = t - seg * J.tiles_x;
-    const int TW = J.tw;
+    const int TW = TWC ? TWC : J.tw;
     const int x0 = tx * TW, nx = min(TW, J.dw - x0);
     const int c0 = J.tile_c0[tx], cn = J.tile_cn[tx];
     const int S = J.S, mask = J.ring - 1;
@@ -159,10 +162,12 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     uint8_t *dbase = a.dst[p] + frame * a.dfs[p];
 
     // horizontal-pass lane mapping: one output column per lane, r_step rows at a time
-    const int col = tid % TW, r_first = tid / TW, r_step = kThreads / TW;
+    const int col = TWC ? tid : tid % TW, r_first = TWC ? 0 : tid / TW, r_step = TWC ? 1 : kThreads / TW;
     // taps as packed 16-bit pairs for v_dot2_i32_i16 (HT is 1 or even)
     constexpr int HP = HT == 1 ? 1 : HT / 2;
     v2i16 hcp[HP];
+#pragma unroll
+    for (int j = 0; j < HP; ++j) hcp[j] = v2i16{0, 0};
     int hbias = 0;  // 32768 * sum(coef): undoes the staging bias of 16-bit samples
     int hoff = 0;
     if (col < nx) {
@@ -185,10 +190,11 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     }
     // vertical-pass lane mapping: 4 adjacent outputs per lane
     const int groups = TW / 4;
-    const int lane_g = tid % groups, row_first = tid / groups, row_step = kThreads / groups;
+    const int lane_g = TWC ? (tid & 63) : tid % groups, row_first = TWC ? (tid >> 6) : tid / groups,
+              row_step = TWC ? 4 : kThreads / groups;
     const int cx = lane_g * 4;
     const int vtp = J.vtp;
-    const int twl = J.twl;
+    const int twl = TWC ? 8 : J.twl;
     const int rbytes_mask = (J.ring << (twl + 1)) - 1;  // ring bytes - 1
 
     const int y_begin = seg * J.seg_h, y_end = min(J.dh, y_begin + J.seg_h);
@@ -209,13 +215,30 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
         const int off = (from + r) * (int)sls + cbyte + ch * 16;
         return id < total ? off : kOobOff;
     };
-    // issue the loads of chunk rows [from, hi) for this lane (first kPF * 256
-    // chunks); straight-line code, so the kPF loads are all in flight at once
+    // staging coordinates, fixed per lane when a row has <= 256 chunks: chunk
+    // column s_ch of rows s_r0, s_r0 + s_rstep, ... (no division per chunk)
+    const bool fixed = cpr <= kThreads;
+    const int s_rstep = fixed ? kThreads / cpr : 1;
+    const int s_r0 = fixed ? tid / cpr : 0, s_ch = fixed ? tid - s_r0 * cpr : 0;
+    const bool s_on = fixed && s_r0 < s_rstep;
+    const int s_lds = s_r0 * S + s_ch * CH;            // LDS sample offset of the lane's first row
+    const int s_goff = s_r0 * (int)sls + cbyte + s_ch * 16;  // its byte offset within the plane, less `from` rows
+    // issue the loads of chunk rows [from, hi) for this lane (first kPF rows of
+    // its column); straight-line code, so the kPF loads are all in flight at once
     auto prefetch = [&](Prefetch<ST> &pf, int from, int hi_) {
         if (!vec) return;
-        const int total = (hi_ - from) * cpr;
+        if (fixed) {
+            const int nrow = hi_ - from;
 #pragma unroll
-        for (int k = 0; k < kPF; ++k) pf.v[k] = bload16(rs, chunk_off(tid + k * kThreads, from, total));
+            for (int k = 0; k < kPF; ++k) {
+                const int r = s_r0 + k * s_rstep;
+                pf.v[k] = bload16(rs, (s_on && r < nrow) ? s_goff + (from + k * s_rstep) * (int)sls : kOobOff);
+            }
+        } else {
+            const int total = (hi_ - from) * cpr;
+#pragma unroll
+            for (int k = 0; k < kPF; ++k) pf.v[k] = bload16(rs, chunk_off(tid + k * kThreads, from, total));
+        }
     };
     // write the prefetched chunks to LDS and stage any remainder synchronously
     auto commit = [&](const Prefetch<ST> &pf, int from, int hi_) {
@@ -227,6 +250,16 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
                                                            (int64_t)(from + r) * sls);
                 store16<ST>(src_t + r * S + ch * CH, load16_scalar<ST>(g, c0 + ch * CH, sw));
             }
+            return;
+        }
+        if (fixed) {
+            const int nrow = hi_ - from;
+            if (!s_on) return;
+#pragma unroll
+            for (int k = 0; k < kPF; ++k)
+                if (s_r0 + k * s_rstep < nrow) store16<ST>(src_t + s_lds + k * s_rstep * S, pf.v[k]);
+            for (int k = kPF; s_r0 + k * s_rstep < nrow; ++k)
+                store16<ST>(src_t + s_lds + k * s_rstep * S, bload16(rs, s_goff + (from + k * s_rstep) * (int)sls));
             return;
         }
 #pragma unroll
@@ -265,7 +298,9 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
             for (int i = tid; i < ny_c; i += kThreads) vpl[i] = J.vbase[y0 + i];
         }
         // ---- horizontal pass into the ring --------------------------------------
-        if (nnew > 0 && col < nx) {
+        // (TWC: lanes past the strip's last column compute with zero taps and
+        // write ring columns the vertical pass never reads -- no divergence)
+        if (nnew > 0 && (TWC || col < nx)) {
             // 4-B aligned dword reads (2-B aligned ones stall the LDS); an odd
             // window start takes each sample pair from two dwords with v_alignbit
             const int odd = hoff & 1;
@@ -419,20 +454,25 @@ __global__ __launch_bounds__(256) void interleave_uyvy_kernel(const uint8_t *Y, 
 
 using KernelFn = void (*)(const ScaleArgs);
 
-template <typename ST, int OUTB>
-KernelFn pick_ht(int ht) {
+template <typename ST, int OUTB, int TWC>
+KernelFn pick_ht_tw(int ht) {
     switch (ht) {
-    case 1: return scale_kernel<ST, OUTB, 1>;
-    case 2: return scale_kernel<ST, OUTB, 2>;
-    case 4: return scale_kernel<ST, OUTB, 4>;
-    case 6: return scale_kernel<ST, OUTB, 6>;
-    case 8: return scale_kernel<ST, OUTB, 8>;
-    case 12: return scale_kernel<ST, OUTB, 12>;
-    case 16: return scale_kernel<ST, OUTB, 16>;
-    case 24: return scale_kernel<ST, OUTB, 24>;
-    case 32: return scale_kernel<ST, OUTB, 32>;
+    case 1: return scale_kernel<ST, OUTB, 1, TWC>;
+    case 2: return scale_kernel<ST, OUTB, 2, TWC>;
+    case 4: return scale_kernel<ST, OUTB, 4, TWC>;
+    case 6: return scale_kernel<ST, OUTB, 6, TWC>;
+    case 8: return scale_kernel<ST, OUTB, 8, TWC>;
+    case 12: return scale_kernel<ST, OUTB, 12, TWC>;
+    case 16: return scale_kernel<ST, OUTB, 16, TWC>;
+    case 24: return scale_kernel<ST, OUTB, 24, TWC>;
+    case 32: return scale_kernel<ST, OUTB, 32, TWC>;
     default: return nullptr;
     }
+}
+
+template <typename ST, int OUTB>
+KernelFn pick_ht(int ht, bool tw256) {
+    return tw256 ? pick_ht_tw<ST, OUTB, kTileW>(ht) : pick_ht_tw<ST, OUTB, 0>(ht);
 }
 
 inline int ht_bucket(int t) {
@@ -757,11 +797,12 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
         a.vec_src &= aligned(a.src[p], a.sls[p], nframes > 1 ? a.sfs[p] : 0, 16);
         a.vec_dst &= aligned(a.dst[p], a.dls[p], nframes > 1 ? a.dfs[p] : 0, out_depth == 8 ? 4 : 8);
     }
+    const bool tw256 = P->job[0].tw == kTileW && P->job[1].tw == kTileW && P->job[2].tw == kTileW;
     KernelFn k;
     if (P->si.depth == 8)
-        k = out_depth == 8 ? pick_ht<uint8_t, 8>(P->ht) : pick_ht<uint8_t, 10>(P->ht);
+        k = out_depth == 8 ? pick_ht<uint8_t, 8>(P->ht, tw256) : pick_ht<uint8_t, 10>(P->ht, tw256);
     else
-        k = out_depth == 8 ? pick_ht<uint16_t, 8>(P->ht) : pick_ht<uint16_t, 10>(P->ht);
+        k = out_depth == 8 ? pick_ht<uint16_t, 8>(P->ht, tw256) : pick_ht<uint16_t, 10>(P->ht, tw256);
     if (!k) PP_FAIL(PP_ERR_UNSUPPORTED, "no kernel for %d taps", P->ht);
     const int tiles = P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y;
     a.tiles = tiles;

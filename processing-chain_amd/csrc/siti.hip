@@ -36,6 +36,7 @@ constexpr int kBand = 16;
 constexpr int kLanePx = 8;
 constexpr int kWaveSpan = 62 * kLanePx;  // 496 px per wave: lanes 0 and 63 are halo lanes
 constexpr int kSpan = 4 * kWaveSpan;     // 1984 px per workgroup
+constexpr int kOob = kOobOff;
 
 struct SitiPartial {
     double mean;   // mean of |G| over n samples
@@ -57,29 +58,6 @@ __device__ inline void chan_merge(int64_t &n, double &mean, double &m2, int64_t 
     m2 += m2b + delta * delta * static_cast<double>(n) * fb;
     n = nn;
 }
-
-template <typename T>
-__device__ inline void load_row(int v[kLanePx], const T *row, int x, int W, bool vec) {
-    if (vec && x + kLanePx <= W) {
-        if constexpr (sizeof(T) == 2) {
-            const uint4 q = *reinterpret_cast<const uint4 *>(row + x);
-            v[0] = q.x & 0xffff; v[1] = q.x >> 16; v[2] = q.y & 0xffff; v[3] = q.y >> 16;
-            v[4] = q.z & 0xffff; v[5] = q.z >> 16; v[6] = q.w & 0xffff; v[7] = q.w >> 16;
-        } else {
-            const uint2 q = *reinterpret_cast<const uint2 *>(row + x);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                v[e] = (q.x >> (8 * e)) & 0xff;
-                v[4 + e] = (q.y >> (8 * e)) & 0xff;
-            }
-        }
-    } else {
-#pragma unroll
-        for (int e = 0; e < kLanePx; ++e) v[e] = (x + e < W) ? static_cast<int>(row[x + e]) : 0;
-    }
-}
-
-constexpr int kOob = kOobOff;
 
 __device__ inline uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
@@ -120,17 +98,42 @@ __device__ inline void issue_row(Row<T> &r, __amdgpu_buffer_rsrc_t rs, int off) 
     }
 }
 
-// Unaligned fallback: element loads, zero outside [0, W) and outside the frame.
+typedef int16_t v2i16 __attribute__((ext_vector_type(2)));
+typedef uint16_t v2u16 __attribute__((ext_vector_type(2)));
+typedef float v2f32 __attribute__((ext_vector_type(2)));
+
+// packed 16-bit lane-pair arithmetic (v_pk_add_u16 / v_pk_sub_i16)
+__device__ inline uint32_t pk_add(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u16, a) + __builtin_bit_cast(v2u16, b));
+}
+__device__ inline uint32_t pk_sub(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2i16, a) - __builtin_bit_cast(v2i16, b));
+}
+// 2 * a + b per 16-bit half (v_pk_mad_u16; wraps like the int16 values it holds)
+__device__ inline uint32_t pk_2a_plus_b(uint32_t a, uint32_t b) {
+    const v2u16 two = {2, 2};
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u16, a) * two + __builtin_bit_cast(v2u16, b));
+}
+// gx^2 + gy^2 of one (gx, gy) pair: the VOP3P form with an inline-constant
+// accumulator (the compiler's v_dot2c form needs a zeroed destination copy)
+__device__ inline int sq_norm(v2i16 p) {
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %1, 0" : "=v"(r) : "v"(p));
+    return r;
+}
+__device__ inline v2f32 pk_fma(v2f32 a, v2f32 b, v2f32 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// A lane's 8 pixels as four u16 pairs (v[2k], v[2k+1]).
 template <typename T>
-__device__ inline void load_row_slow(Row<T> &r, const uint8_t *frame, int64_t ls, int row, int H, int x, int W) {
-    int v[kLanePx] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (frame && row >= 0 && row < H) load_row<T>(v, reinterpret_cast<const T *>(frame + (int64_t)row * ls), x, W, false);
+__device__ inline void to_pairs(const Row<T> &r, uint32_t w[4]) {
+    if constexpr (sizeof(T) == 2) {
 #pragma unroll
-    for (int i = 0; i < Row<T>::N; ++i) r.w[i] = 0;
-#pragma unroll
-    for (int e = 0; e < kLanePx; ++e) {
-        if constexpr (sizeof(T) == 2) r.w[e >> 1] |= (uint32_t)v[e] << (16 * (e & 1));
-        else r.w[e >> 2] |= (uint32_t)v[e] << (8 * (e & 3));
+        for (int k = 0; k < 4; ++k) w[k] = r.w[k];
+    } else {
+        w[0] = __builtin_amdgcn_perm(0u, r.w[0], 0x0c010c00u);
+        w[1] = __builtin_amdgcn_perm(0u, r.w[0], 0x0c030c02u);
+        w[2] = __builtin_amdgcn_perm(0u, r.w[1], 0x0c010c00u);
+        w[3] = __builtin_amdgcn_perm(0u, r.w[1], 0x0c030c02u);
     }
 }
 
@@ -140,7 +143,7 @@ __device__ inline void load_row_slow(Row<T> &r, const uint8_t *frame, int64_t ls
 // flight while the current one is computed, with no extra registers and no
 // branches around the loads.  The previous frame's band (TI) stays in
 // registers too, so every pixel is read from HBM once (plus the two halo rows).
-template <typename T, bool VEC>
+template <typename T>
 __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_t ls, int64_t fs, int nframes,
                                                    const uint8_t *prev, int W, int H, int tiles_x, int bands,
                                                    int chunk, SitiPartial *part) {
@@ -159,9 +162,6 @@ __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_
     const int x = tx * kSpan + wave * kWaveSpan + (lane - 1) * kLanePx;
     const bool halo = lane == 0 || lane == 63;
     const int y0 = band * kBand, y1 = min(H, y0 + kBand);
-    int valid_px = 0;  // pixels this lane accounts for (TI)
-#pragma unroll
-    for (int e = 0; e < kLanePx; ++e) valid_px += (!halo && x + e >= 0 && x + e < W);
     // lane-relative valid Sobel columns [lo, hi] (empty for halo lanes)
     const int sobel_lo = halo ? kLanePx : 1 - x, sobel_hi = halo ? -1 : W - 2 - x;
 
@@ -182,8 +182,7 @@ __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_
         const auto prs = rsrc(have_pfirst ? pfirst : frames);
 #pragma unroll
         for (int i = 0; i < kBand; ++i) {
-            if constexpr (VEC) issue_row<T>(pv[i], prs, row_off(y0 + i, have_pfirst && y0 + i < y1));
-            else load_row_slow<T>(pv[i], have_pfirst && x_in && y0 + i < y1 ? pfirst : nullptr, ls, y0 + i, H, x, W);
+            issue_row<T>(pv[i], prs, row_off(y0 + i, have_pfirst && y0 + i < y1));
         }
     }
     // first frame's window
@@ -194,10 +193,26 @@ __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_
 #pragma unroll
         for (int ri = 0; ri < NR; ++ri) {
             const int r = y0 - 1 + ri;
-            if constexpr (VEC) issue_row<T>(raw[ri], crs, row_off(r, live));
-            else load_row_slow<T>(raw[ri], live && x_in ? fb : nullptr, ls, r, H, x, W);
+            issue_row<T>(raw[ri], crs, row_off(r, live));
         }
     }
+
+    // per-lane constants of the packed formulation
+    uint32_t tmask[4];  // TI: 0xffff per pixel this lane accounts for
+    v2f32 vm[4];        // Sobel: 1.0 per valid Sobel column, else 0
+    int rc = 0;         // valid Sobel columns of this lane
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int e0 = 2 * k, e1 = 2 * k + 1;
+        const bool t0 = !halo && x + e0 >= 0 && x + e0 < W, t1 = !halo && x + e1 >= 0 && x + e1 < W;
+        tmask[k] = (t0 ? 0xffffu : 0u) | (t1 ? 0xffff0000u : 0u);
+        const bool s0 = e0 >= sobel_lo && e0 <= sobel_hi, s1 = e1 >= sobel_lo && e1 <= sobel_hi;
+        vm[k] = v2f32{s0 ? 1.f : 0.f, s1 ? 1.f : 0.f};
+        rc += s0 + s1;
+    }
+    const float frc = static_cast<float>(rc);
+    const float inv_rc = rc ? 1.f / frc : 0.f;
+    const uint32_t ones = 0x00010001u;
 
     for (int f = f0; f < f1; ++f) {
         const bool has_prev = f > 0 || prev != nullptr;
@@ -205,97 +220,107 @@ __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_
         const uint8_t *nb = frames + (int64_t)(nlive ? f + 1 : f) * fs;
         const auto nrs = rsrc(nb);
         float n_t = 0.f, mean_t = 0.f, m2_t = 0.f;
-        uint64_t d2s = 0;
-        int64_t d1s = 0;
-        int h1a[kLanePx], h2a[kLanePx], h1b[kLanePx], h2b[kLanePx];
+        int d1s = 0;        // |sum d| <= 16 rows * 8 px * 1023
+        uint32_t d2s = 0;   // sum d^2 <= 16 * 8 * 1023^2 < 2^32
+        uint32_t h1a[4], h2a[4], h1b[4], h2b[4];  // packed int16 pairs of the rows above
 #pragma unroll
         for (int ri = 0; ri < NR; ++ri) {
             const int r = y0 - 1 + ri;
-            int v[kLanePx];
+            uint32_t w[4];
+            to_pairs<T>(raw[ri], w);
+            // neighbours: the last pixel of the lane below, the first of the lane above
+            // (DPP wave shifts; only halo lanes see the wave's ends)
+            const uint32_t wl = __builtin_amdgcn_mov_dpp(w[3], 0x138, 0xf, 0xf, true);  // wave_shr:1
+            const uint32_t wr = __builtin_amdgcn_mov_dpp(w[0], 0x130, 0xf, 0xf, true);  // wave_shl:1
+            uint32_t h1[4], h2[4];
 #pragma unroll
-            for (int e = 0; e < kLanePx; ++e) v[e] = raw[ri].px(e);
-            int h1[kLanePx], h2[kLanePx];
-            {
-                const int left = __shfl_up(v[kLanePx - 1], 1, 64);   // garbage only on halo lanes
-                const int right = __shfl_down(v[0], 1, 64);
-#pragma unroll
-                for (int e = 0; e < kLanePx; ++e) {
-                    const int l = e ? v[e - 1] : left;
-                    const int rr = e < kLanePx - 1 ? v[e + 1] : right;
-                    h1[e] = rr - l;
-                    h2[e] = l + 2 * v[e] + rr;
-                }
+            for (int k = 0; k < 4; ++k) {
+                // (v[2k-1], v[2k]) and (v[2k+1], v[2k+2]) as u16 pairs
+                const uint32_t lp = __builtin_amdgcn_alignbit(w[k], k ? w[k - 1] : wl, 16);
+                const uint32_t rp = __builtin_amdgcn_alignbit(k < 3 ? w[k + 1] : wr, w[k], 16);
+                h1[k] = pk_sub(rp, lp);                    // right - left         (|.| <= 1023)
+                h2[k] = pk_add(pk_2a_plus_b(w[k], lp), rp);  // left + 2 v + right (<= 4092)
             }
             // TI on the band rows against the previous frame's band
             const int bi = ri - 1;
             if (ri >= 1 && ri <= kBand) {
                 if (has_prev && r < y1) {
-                    int ds = 0;
-                    uint32_t dq = 0;
+                    uint32_t q[4];
+                    to_pairs<T>(pv[bi], q);
 #pragma unroll
-                    for (int e = 0; e < kLanePx; ++e) {
-                        const int d = (e < valid_px) ? v[e] - pv[bi].px(e) : 0;
-                        ds += d;
-                        dq += static_cast<uint32_t>(d * d);
+                    for (int k = 0; k < 4; ++k) {
+                        const v2i16 d = __builtin_bit_cast(v2i16, pk_sub(w[k], q[k]) & tmask[k]);
+                        d1s = __builtin_amdgcn_sdot2(d, __builtin_bit_cast(v2i16, ones), d1s, false);
+                        d2s = static_cast<uint32_t>(__builtin_amdgcn_sdot2(d, d, static_cast<int>(d2s), false));
                     }
-                    d1s += ds;
-                    d2s += dq;
                 }
                 pv[bi] = raw[ri];
             }
             // Sobel centred on row c = r - 1 (rows c-1, c, c+1 are in the window)
             const int c = r - 1;
             if (ri >= 2 && c < y1 && c >= 1 && c <= H - 2) {
-                float mag[kLanePx];
-                float rs = 0.f;
-                int rc = 0;
+                v2f32 mag[4];
 #pragma unroll
-                for (int e = 0; e < kLanePx; ++e) {
-                    const int gx = h1a[e] + 2 * h1b[e] + h1[e];
-                    const int gy = h2[e] - h2a[e];
-                    const bool ok = e >= sobel_lo && e <= sobel_hi;
-                    mag[e] = ok ? __fsqrt_rn(static_cast<float>(gx * gx + gy * gy)) : 0.f;
-                    rs += mag[e];
-                    rc += ok;
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t gx = pk_add(pk_2a_plus_b(h1b[k], h1a[k]), h1[k]);  // |.| <= 4092
+                    const uint32_t gy = pk_sub(h2[k], h2a[k]);
+                    // (gx, gy) of each pixel as one pair: |G|^2 = dot2(p, p)
+                    const v2i16 p0 = __builtin_bit_cast(v2i16, __builtin_amdgcn_perm(gy, gx, 0x05040100u));
+                    const v2i16 p1 = __builtin_bit_cast(v2i16, __builtin_amdgcn_perm(gy, gx, 0x07060302u));
+                    const int g0 = sq_norm(p0), g1 = sq_norm(p1);
+                    mag[k] = v2f32{__fsqrt_rn(static_cast<float>(g0)), __fsqrt_rn(static_cast<float>(g1))};
                 }
-                if (rc) {
-                    const float rm = rs / static_cast<float>(rc);
-                    float rm2 = 0.f;
+                // per-row two-pass statistics over the lane's valid columns (exact 0
+                // for a constant row), merged into the lane's running (n, mean, M2)
+                v2f32 sv = mag[0] * vm[0];
 #pragma unroll
-                    for (int e = 0; e < kLanePx; ++e) {
-                        const float dv = mag[e] - rm;
-                        rm2 += (e >= sobel_lo && e <= sobel_hi) ? dv * dv : 0.f;
-                    }
-                    chan_merge_f(n_t, mean_t, m2_t, static_cast<float>(rc), rm, rm2);
+                for (int k = 1; k < 4; ++k) sv = pk_fma(mag[k], vm[k], sv);
+                const float rm = (sv.x + sv.y) * inv_rc;
+                const v2f32 nrm = {-rm, -rm};
+                v2f32 qv = {0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const v2f32 dv = (mag[k] + nrm) * vm[k];
+                    qv = pk_fma(dv, dv, qv);
                 }
+                const float rm2 = qv.x + qv.y;
+                const float nn = n_t + frc;
+                const float fb = frc * __builtin_amdgcn_rcpf(nn > 0.f ? nn : 1.f);
+                const float delta = rm - mean_t;
+                mean_t += delta * fb;
+                m2_t += rm2 + delta * delta * n_t * fb;
+                n_t = nn;
             }
 #pragma unroll
-            for (int e = 0; e < kLanePx; ++e) {
-                h1a[e] = h1b[e]; h2a[e] = h2b[e];
-                h1b[e] = h1[e]; h2b[e] = h2[e];
+            for (int k = 0; k < 4; ++k) {
+                h1a[k] = h1b[k]; h2a[k] = h2b[k];
+                h1b[k] = h1[k]; h2b[k] = h2[k];
             }
             // this row is consumed: start loading the next frame's row ri into it
-            if constexpr (VEC) issue_row<T>(raw[ri], nrs, row_off(r, nlive));
-            else load_row_slow<T>(raw[ri], nlive && x_in ? nb : nullptr, ls, r, H, x, W);
+            issue_row<T>(raw[ri], nrs, row_off(r, nlive));
         }
-        // wave reduction (fixed order, fp64) -> one partial per (frame, tile, wave)
-        int64_t cnt = static_cast<int64_t>(n_t);
-        double mean = mean_t, m2 = m2_t;
+        // wave reduction in fp64, fixed butterfly order: N, sum n*mean -> mean_w,
+        // then sum (M2 + n (mean - mean_w)^2); TI moments as integers
+        double cnt = n_t, sum = static_cast<double>(n_t) * static_cast<double>(mean_t);
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
-            const int64_t nb2 = __shfl_xor(cnt, o, 64);
-            const double mb = __shfl_xor(mean, o, 64), qb = __shfl_xor(m2, o, 64);
-            // both lanes of a pair merge (lower, upper) in the same order
-            if ((lane & o) == 0) chan_merge(cnt, mean, m2, nb2, mb, qb);
-            else {
-                int64_t n2 = nb2; double mm = mb, qq = qb;
-                chan_merge(n2, mm, qq, cnt, mean, m2);
-                cnt = n2; mean = mm; m2 = qq;
-            }
+            cnt += __shfl_xor(cnt, o, 64);
+            sum += __shfl_xor(sum, o, 64);
         }
-        d1s = static_cast<int64_t>(wave_sum_u64(static_cast<uint64_t>(d1s)));
-        d2s = wave_sum_u64(d2s);
-        if (lane == 0) part[((int64_t)f * tiles_x * bands + tile) * 4 + wave] = {mean, m2, cnt, d1s, d2s, 0};
+        const double mean_w = cnt > 0.0 ? sum / cnt : 0.0;
+        const double dm = static_cast<double>(mean_t) - mean_w;
+        double m2 = static_cast<double>(m2_t) + static_cast<double>(n_t) * dm * dm;
+        int64_t d1 = d1s;
+        uint64_t d2 = d2s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            m2 += __shfl_xor(m2, o, 64);
+            d1 += __shfl_xor(d1, o, 64);
+            d2 += __shfl_xor(d2, o, 64);
+        }
+        if (lane == 0)
+            part[((int64_t)f * tiles_x * bands + tile) * 4 + wave] = {mean_w, m2, static_cast<int64_t>(cnt), d1,
+                                                                       d2, 0};
     }
 }
 
@@ -359,26 +384,52 @@ extern "C" int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma
     int dev_cus = 0, per_cu = 0;
     PP_HIP(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     PP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, bytes == 2 ? (const void *)siti_kernel<uint16_t, true> : (const void *)siti_kernel<uint8_t, true>, 256, 0));
+        &per_cu, bytes == 2 ? (const void *)siti_kernel<uint16_t> : (const void *)siti_kernel<uint8_t>, 256, 0));
     const int slots = std::max(1, dev_cus * std::max(1, per_cu));
     int chunks = std::max(1, slots / ntiles);
     if (chunks > nframes) chunks = nframes;
     const int chunk = (nframes + chunks - 1) / chunks;
     chunks = (nframes + chunk - 1) / chunk;
+    // The kernel reads each lane's 8 pixels as one 16-B (8-B) buffer load, so
+    // rows must start on that granule; other layouts (odd widths packed
+    // contiguously, views into a row) are first repacked on the device into a
+    // pitched scratch copy -- one extra read+write, never a second code path.
     const int a = bytes == 2 ? 16 : 8;
-    const int vec = ((uintptr_t)luma % a == 0) && (linesize % a == 0) && (nframes < 2 || frame_stride % a == 0) &&
-                    (!prev || (uintptr_t)prev % a == 0) &&
-                    ((int64_t)(h - 1) * linesize + (int64_t)w * bytes < (int64_t)kOob);
+    const bool aligned = ((uintptr_t)luma % a == 0) && (linesize % a == 0) && (nframes < 2 || frame_stride % a == 0) &&
+                         (!prev || (uintptr_t)prev % a == 0);
+    const uint8_t *src = static_cast<const uint8_t *>(luma), *psrc = static_cast<const uint8_t *>(prev);
+    int64_t ls = linesize, fs = frame_stride;
+    uint8_t *scratch = nullptr;
+    if (!aligned) {
+        ls = ((int64_t)w * bytes + 15) & ~int64_t(15);
+        fs = ls * h;
+        const int nf = nframes + (prev ? 1 : 0);
+        PP_HIP(hipMallocAsync((void **)&scratch, (size_t)(fs * nf), st));
+        uint8_t *dst = scratch + (prev ? fs : 0);
+        if (nframes == 1 || frame_stride == linesize * h) {
+            PP_HIP(hipMemcpy2DAsync(dst, ls, luma, linesize, (size_t)w * bytes, (size_t)h * nframes,
+                                    hipMemcpyDeviceToDevice, st));
+        } else {
+            for (int f = 0; f < nframes; ++f)
+                PP_HIP(hipMemcpy2DAsync(dst + f * fs, ls, static_cast<const uint8_t *>(luma) + f * frame_stride,
+                                        linesize, (size_t)w * bytes, h, hipMemcpyDeviceToDevice, st));
+        }
+        if (prev)
+            PP_HIP(hipMemcpy2DAsync(scratch, ls, prev, linesize, (size_t)w * bytes, h, hipMemcpyDeviceToDevice, st));
+        src = dst;
+        psrc = prev ? scratch : nullptr;
+    }
+    if ((int64_t)(h - 1) * ls + (int64_t)w * bytes >= (int64_t)kOob)
+        PP_FAIL(PP_ERR_UNSUPPORTED, "frame of %lld bytes exceeds the 2 GiB buffer range", (long long)(h * ls));
     SitiPartial *part = nullptr;
     PP_HIP(hipMallocAsync((void **)&part, sizeof(SitiPartial) * (size_t)ntiles * 4 * nframes, st));
     dim3 grid(ntiles * chunks);
-    auto k = bytes == 2 ? (vec ? siti_kernel<uint16_t, true> : siti_kernel<uint16_t, false>)
-                        : (vec ? siti_kernel<uint8_t, true> : siti_kernel<uint8_t, false>);
-    hipLaunchKernelGGL(k, grid, dim3(256), 0, st, (const uint8_t *)luma, linesize, frame_stride, nframes,
-                       (const uint8_t *)prev, w, h, tiles_x, bands, chunk, part);
+    auto k = bytes == 2 ? siti_kernel<uint16_t> : siti_kernel<uint8_t>;
+    hipLaunchKernelGGL(k, grid, dim3(256), 0, st, src, ls, fs, nframes, psrc, w, h, tiles_x, bands, chunk, part);
     hipLaunchKernelGGL(siti_finalize, dim3(nframes), dim3(256), 0, st, part, nframes, ntiles * 4, w, h,
                        prev != nullptr, si, ti);  // ntiles * 4 wave partials per frame
     PP_HIP(hipGetLastError());
     PP_HIP(hipFreeAsync(part, st));
+    if (scratch) PP_HIP(hipFreeAsync(scratch, st));
     return PP_OK;
 }

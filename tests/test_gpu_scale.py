@@ -91,3 +91,28 @@ def test_scale_large_batch_consistency(gpu):
         v = dst.view(p)
         assert torch.equal(v, v[:1].expand_as(v)), "frames of the batch differ"
         assert np.array_equal(v[n - 1].cpu().numpy(), ref[p])
+
+
+@pytest.mark.parametrize("case", [
+    (po.YUV420P, 333, 197, po.YUV420P, 500, 301, po.SWS_BICUBIC),
+    (po.YUV420P10LE, 250, 99, po.YUV422P10LE, 641, 363, po.SWS_LANCZOS),
+], ids=["8bit-ragged", "10bit-ragged"])
+def test_scale_interleaved_unaligned_source(gpu, case):
+    """Frame-interleaved dense Y|U|V input (the raw pipe layout): odd widths
+    give unaligned rows, which take the element-wise staging path."""
+    import torch
+    from pixpath import ops
+    from pixpath.frames import FrameBatch
+    sf, sw, sh, df, dw, dh, flags = case
+    n = 3
+    frames = _frames("noise", sf, sw, sh, n, seed=11)
+    src = FrameBatch.interleaved(sf, sw, sh, n, device=gpu)
+    for p in range(3):
+        src.planes[p].copy_(torch.from_numpy(np.stack([f[p] for f in frames])).to(gpu))
+    assert src.frames_struct().linesize[0] % 16 != 0
+    out = ops.Scaler(sf, sw, sh, df, dw, dh, flags=flags)(src).to_numpy()
+    torch.cuda.synchronize()
+    for i in range(n):
+        ref = po.scale(sf, frames[i], df, dw, dh, flags)
+        for p, r in enumerate(ref):
+            assert np.array_equal(out[p][i], r), "frame %d plane %d" % (i, p)
