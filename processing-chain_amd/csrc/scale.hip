@@ -46,7 +46,7 @@ struct PlaneJob {
     int sw, sh, dw, dh;
     int tiles_x, tiles_y, tile_base;  // strips x vertical segments, first block index
     int tw, twl, seg_h, cho; // strip width (= 1 << twl), output rows per segment, output rows per chunk
-    int vtp, ring, maxnew, S; // V tap pairs, ring rows (pow2, >= 2), staged rows per chunk, staged cols
+    int vtp, ring, maxnew, S; // V tap pairs, window rows (even), staged rows per chunk, staged cols
     int dither_off;       // 0 (Y, U) or 3 (V)
     const int32_t *hpos;  // [dw]   window start (absolute source column)
     const int16_t *hcoef; // [dw * HT]
@@ -106,6 +106,14 @@ __device__ inline uint4 bload16(__amdgpu_buffer_rsrc_t rs, int off) {
 
 typedef int16_t v2i16 __attribute__((ext_vector_type(2)));
 
+// a.lo*b.lo + a.hi*b.hi + c in the VOP3P form (the compiler's v_dot2c form
+// needs the accumulator copied into the destination first)
+__device__ inline int dot2_acc(v2i16 a, v2i16 b, int c) {
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // 16-bit sources are stored as s ^ 0x8000 (= s - 32768 as int16) so any u16
 // sample is an exact signed operand of v_dot2_i32_i16; the H pass adds the
 // 32768 * sum(coef) bias back.  8-bit samples are stored as-is (<= 255).
@@ -150,11 +158,14 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     const int TW = TWC ? TWC : J.tw;
     const int x0 = tx * TW, nx = min(TW, J.dw - x0);
     const int c0 = J.tile_c0[tx], cn = J.tile_cn[tx];
-    const int S = J.S, mask = J.ring - 1;
+    const int S = J.S;
     uint16_t *src_t = lds;                                              // [maxnew][S]
-    // ring of 15-bit intermediates, row pairs interleaved per column:
-    // element (row R, col c) at [((R & mask) >> 1) * TW + c] * 2 + (R & 1)
+    // window of 15-bit intermediates, row pairs interleaved per column: the
+    // dword [k][c] holds rows (base + 2k, base + 2k + 1) of column c, base = the
+    // chunk's first source row rounded down to even (rows a chunk shares with
+    // the previous one are moved down at the chunk start, so reads never wrap)
     int16_t *ring = reinterpret_cast<int16_t *>(lds + J.maxnew * S);
+    uint32_t *win = reinterpret_cast<uint32_t *>(ring);
     int32_t *vcl = reinterpret_cast<int32_t *>(ring + J.ring * TW);     // [cho][vtp] chunk V tap pairs
     int32_t *vpl = vcl + J.cho * J.vtp;                                  // [cho] chunk V base rows
     const int tid = threadIdx.x;
@@ -194,8 +205,7 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
               row_step = TWC ? 4 : kThreads / groups;
     const int cx = lane_g * 4;
     const int vtp = J.vtp;
-    const int twl = TWC ? 8 : J.twl;
-    const int rbytes_mask = (J.ring << (twl + 1)) - 1;  // ring bytes - 1
+    (void)J.twl;
 
     const int y_begin = seg * J.seg_h, y_end = min(J.dh, y_begin + J.seg_h);
     constexpr int CH = 16 / sizeof(ST);
@@ -277,16 +287,44 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     };
 
     int next_src = J.chunk_lo[y_begin / J.cho];
+    int base = next_src & ~1;  // window row 0 (even source row)
     Prefetch<ST> pf;
     // rows the first chunk needs
     int pf_from = next_src, pf_hi = J.chunk_hi[y_begin / J.cho];
     if (pf_from < J.chunk_lo[y_begin / J.cho]) pf_from = J.chunk_lo[y_begin / J.cho];
     prefetch(pf, pf_from, pf_hi);
+    // one H-pass output row: taps over the staged source row at `sp` (window
+    // start hoff, 4-B aligned reads, odd starts re-paired with v_alignbit)
+    const int odd = hoff & 1;
+    const uint32_t ash = odd * 16;
+    auto hrow = [&](const uint16_t *sp) -> uint32_t {
+        int acc;
+        if constexpr (HT == 1) {
+            acc = hbias + static_cast<int>(static_cast<int16_t>(sp[odd])) * hcp[0][0];
+        } else {
+            const uint32_t *sw32 = static_cast<const uint32_t *>(__builtin_assume_aligned(sp, 4));
+            uint32_t w[HP + 1];
+#pragma unroll
+            for (int j = 0; j <= HP; ++j) w[j] = sw32[j];
+            acc = dot2_acc(__builtin_bit_cast(v2i16, __builtin_amdgcn_alignbit(w[1], w[0], ash)), hcp[0], hbias);
+#pragma unroll
+            for (int j = 1; j < HP; ++j)
+                acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, __builtin_amdgcn_alignbit(w[j + 1], w[j], ash)),
+                                             hcp[j], acc, false);
+        }
+        acc >>= a.hshift;
+        return static_cast<uint32_t>(acc < 32767 ? acc : 32767) & 0xffffu;
+    };
+    const int nxw = TWC ? TW : nx;  // window columns written (TWC: all, harmlessly)
     for (int y0 = y_begin; y0 < y_end; y0 += J.cho) {
         const int ci = y0 / J.cho;
         const int lo = J.chunk_lo[ci], hi = J.chunk_hi[ci];
         if (next_src < lo) next_src = lo;
         const int nnew = hi - next_src;
+        const int nbase = lo & ~1;
+        // rows kept from the previous chunk: [nbase, next_src), as whole pairs
+        const int keep = next_src > nbase ? (next_src - nbase + 1) >> 1 : 0;
+        const int shift = (nbase - base) >> 1;
         // ---- commit the prefetched rows (src_t is not read by the vertical pass) ----
         if (nnew > 0) commit(pf, next_src, hi);
         __syncthreads();  // staged rows visible; every wave has left the previous vertical pass
@@ -295,37 +333,35 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
         {
             const int ny_c = min(J.cho, y_end - y0);
             for (int i = tid; i < ny_c * vtp; i += kThreads) vcl[i] = J.vcoef2[(int64_t)y0 * vtp + i];
-            for (int i = tid; i < ny_c; i += kThreads) vpl[i] = J.vbase[y0 + i];
+            for (int i = tid; i < ny_c; i += kThreads) vpl[i] = J.vbase[y0 + i] - nbase;
         }
-        // ---- horizontal pass into the ring --------------------------------------
+        // ---- move the kept pairs down to the window start: each column by one
+        // lane, in increasing order, so no lane reads a slot already overwritten ----
+        if (shift > 0 && r_first == 0 && col < nxw) {
+            for (int k = 0; k < keep; ++k) win[k * TW + col] = win[(k + shift) * TW + col];
+        }
+        // general strip width: other lanes of the column write new pairs that the
+        // copy may still have to read (TWC: one lane per column, program order)
+        if constexpr (!TWC) __syncthreads();
+        base = nbase;
+        // ---- horizontal pass into the window, one row pair per step -------------
         // (TWC: lanes past the strip's last column compute with zero taps and
-        // write ring columns the vertical pass never reads -- no divergence)
-        if (nnew > 0 && (TWC || col < nx)) {
-            // 4-B aligned dword reads (2-B aligned ones stall the LDS); an odd
-            // window start takes each sample pair from two dwords with v_alignbit
-            const int odd = hoff & 1;
-            const uint32_t ash = odd * 16;
-            const uint16_t *s = src_t + r_first * S + hoff - odd;
-#pragma unroll 4
-            for (int r = r_first; r < nnew; r += r_step) {
-                int acc = hbias;
-                if constexpr (HT == 1) {
-                    acc += static_cast<int>(static_cast<int16_t>(s[odd])) * hcp[0][0];
-                } else {
-                    const uint32_t *sw32 = static_cast<const uint32_t *>(__builtin_assume_aligned(s, 4));
-                    uint32_t w[HP + 1];
-#pragma unroll
-                    for (int j = 0; j <= HP; ++j) w[j] = sw32[j];
-#pragma unroll
-                    for (int j = 0; j < HP; ++j)
-                        acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, __builtin_amdgcn_alignbit(w[j + 1], w[j], ash)),
-                                                     hcp[j], acc, false);
-                }
-                acc >>= a.hshift;
-                const int R = (next_src + r) & mask;
-                // element ((R >> 1) * TW + col) * 2 + (R & 1), TW = 1 << twl
-                ring[(((R & ~1) << twl) | (R & 1)) + 2 * col] = static_cast<int16_t>(acc < 32767 ? acc : 32767);
-                s += r_step * S;
+        // write window columns the vertical pass never reads -- no divergence)
+        if (nnew > 0 && col < nxw) {
+            const int i0 = next_src - base;            // window row of the first new row
+            const uint16_t *sp = src_t + hoff - odd;
+            // a half pair at each end (its other row is kept, or not needed), full
+            // pairs in between: one packed 32-bit write per two rows
+            const int kf0 = (i0 + 1) >> 1, kf1 = (i0 + nnew) >> 1;
+            if ((i0 & 1) && r_first == 0)  // high row of pair i0/2 (same lane as the copy above)
+                reinterpret_cast<uint16_t *>(win + (i0 >> 1) * TW + col)[1] = static_cast<uint16_t>(hrow(sp));
+            if (((i0 + nnew) & 1) && r_first == r_step - 1)  // low row of the last pair
+                reinterpret_cast<uint16_t *>(win + kf1 * TW + col)[0] =
+                    static_cast<uint16_t>(hrow(sp + (nnew - 1) * S));
+            for (int k = kf0 + r_first; k < kf1; k += r_step) {
+                const int ra = 2 * k - i0;             // new-row index of the pair's low row
+                const uint32_t lo16 = hrow(sp + ra * S), hi16 = hrow(sp + (ra + 1) * S);
+                win[k * TW + col] = lo16 | (hi16 << 16);
             }
         }
         if (nnew > 0) next_src = hi;
@@ -342,19 +378,15 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
             if (TW == kTileW) yy = __builtin_amdgcn_readfirstlane(yy);
             if (yy >= ny) break;
             const int y = y0 + yy;
-            // byte offset of row pair vbase/2 in the ring; advancing one pair is
-            // + 4 * TW bytes, wrapped by the (power-of-two) ring size
-            int ro = (vpl[yy] & mask) << (J.twl + 1);
             const int32_t *vc = vcl + yy * vtp;
             if (cx >= nx) continue;
             int acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
-            const uint8_t *rbase = reinterpret_cast<const uint8_t *>(ring) + cx * 4;
+            // pairs (vbase + 2j, vbase + 2j + 1) of columns cx..cx+3: one 16-B read each
+            const uint4 *rp = reinterpret_cast<const uint4 *>(win + (vpl[yy] >> 1) * TW + cx);
 #pragma unroll 2
             for (int j = 0; j < vtp; ++j) {
                 const v2i16 cf = __builtin_bit_cast(v2i16, vc[j]);
-                // rows (2(pb+j), 2(pb+j)+1) of columns cx..cx+3: one 16-B read
-                const uint4 q = *reinterpret_cast<const uint4 *>(rbase + ro);
-                ro = (ro + (4 << J.twl)) & rbytes_mask;
+                const uint4 q = rp[j * (TW / 4)];
                 acc0 = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.x), cf, acc0, false);
                 acc1 = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.y), cf, acc1, false);
                 acc2 = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.z), cf, acc2, false);
@@ -588,10 +620,18 @@ void row_chunks(HostPlane &hp, int sh, int dh, int cho, int seg_h, int *maxnew, 
             next = std::max(next, hp.hi[ci]);
         }
     }
-    int r = 2;  // row pairs: at least one pair
-    while (r < span) r <<= 1;
+    // window rows: from the chunk's even base to its last staged row or the
+    // last row pair its vertical taps read (zero-weight taps included)
+    int wr = 2;
+    for (int ci = 0; ci < nch; ++ci) {
+        const int b = hp.lo[ci] & ~1;
+        int top = hp.hi[ci];
+        for (int y = ci * cho; y < std::min(dh, (ci + 1) * cho); ++y) top = std::max(top, hp.vbase[y] + 2 * hp.vtp);
+        wr = std::max(wr, top - b);
+    }
+    (void)span;
     *maxnew = std::max(mn, 1);
-    *ring = r;
+    *ring = (wr + 1) & ~1;
 }
 
 // Strip width / chunk height / segments for one plane: the widest strip and
