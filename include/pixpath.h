@@ -101,6 +101,12 @@ int pp_scale_plan_destroy(pp_scale_plan *plan);
  * 0 when the plan uses an unscaled converter, or <0. */
 int pp_scale_plan_filter(const pp_scale_plan *plan, int which, int16_t *coef,
                          int32_t *pos, int capacity);
+/* Kernel the plan runs for 16-B aligned sources: > 0 = the strip kernel's
+ * horizontal window in dwords (the common case), 0 = the general kernel
+ * (narrow strips / long vertical filters / unscaled converters).  The
+ * environment variable PIXPATH_SCALE_KERNEL=generic at plan creation forces 0
+ * (parity tests run both kernels on the same cases). */
+int pp_scale_plan_path(const pp_scale_plan *plan);
 /* Run the plan on `nframes` device frames. */
 int pp_scale_execute(pp_scale_plan *plan, const pp_frames *src,
                      const pp_frames *dst, int nframes, void *stream);

@@ -22,8 +22,11 @@
 // three planes of a whole frame batch go in ONE launch
 // (blockIdx.x = strip x segment over the planes, blockIdx.y = frame).
 #include <algorithm>
+#include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <type_traits>
 
 #include "common.hpp"
 #include "device.hpp"
@@ -54,6 +57,10 @@ struct PlaneJob {
     const int32_t *vcoef2; // [dh * vtp] tap pairs (rows base+2j, base+2j+1) packed lo|hi
     const int32_t *tile_c0, *tile_cn; // [tiles_x] staged column window per strip
     const int32_t *chunk_lo, *chunk_hi; // [ceil(dh/cho)] source rows needed by each chunk
+    // strip_kernel only
+    const int32_t *hbase4;  // [tiles_x * 64] 8-B aligned window base (staged-row sample) per 4-column lane
+    const int32_t *hcoefw;  // [tiles_x * 64][4][HW] taps re-laid over the lane's HW dwords (int16 pairs)
+    const int32_t *vrow16;  // [dh][16] per output row: window base row (even), then 8 tap pairs (zero padded)
 };
 
 struct ScaleArgs {
@@ -111,6 +118,14 @@ typedef int16_t v2i16 __attribute__((ext_vector_type(2)));
 __device__ inline int dot2_acc(v2i16 a, v2i16 b, int c) {
     int r;
     asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// a.lo*b.lo + a.hi*b.hi with a zero accumulator as an inline constant (the
+// compiler otherwise zeroes a register for the v_dot2c form)
+__device__ inline int dot2_first(v2i16 a, v2i16 b) {
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
 
@@ -439,6 +454,287 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// strip_kernel: the common-case scaler (every plane in 256-column strips,
+// 16-B aligned source rows, <= 8 vertical tap pairs, <= 10-bit samples).
+//
+// Same strip/segment/chunk walk and LDS layout as scale_kernel, but every
+// loop is wave-uniform (wave = row group, lane = 4 adjacent columns), so the
+// control flow is scalar branches instead of exec-mask bookkeeping:
+//   H pass: one lane computes 4 adjacent output columns of a row PAIR.  The 4
+//     windows share one 8-B aligned base in the staged row (hbase4), read as
+//     HW dwords with ds_read_b64 (one read serves all 4 outputs); per output
+//     the taps are re-laid over those dwords (hcoefw, zero outside its
+//     window), so each output is HW v_dot2_i32_i16 with no realignment, and
+//     the 8 results go to the window as one ds_write_b128.
+//   V pass: a wave owns an output row; its tap pairs come from a padded
+//     [dh][8] table through scalar loads (SGPR operands of v_dot2), the
+//     window rows through ds_read_b128 (4 columns x 2 rows), one 8-B store.
+//   Kept row pairs are read before the chunk's first barrier and written
+//     after it, so the move costs no extra barrier.
+// The next chunk's source rows are prefetched into registers right after the
+// first barrier, so their HBM latency overlaps both passes.
+#define kconst __attribute__((address_space(4)))  // constant address space: uniform loads become s_load
+template <typename T>
+__device__ inline const kconst T *as_kconst(const void *p) {
+    return (const kconst T *)(uintptr_t)p;
+}
+constexpr int kKeepRegs = 2;  // kept pairs per wave carried in registers (4 waves -> 8 pairs)
+
+template <typename ST>
+__device__ inline void store_raw16(uint16_t *lds_dst, uint4 v) {
+    if constexpr (sizeof(ST) == 2) {
+        *reinterpret_cast<uint4 *>(lds_dst) = v;  // <= 10-bit samples are exact int16 operands
+    } else {
+        store16<ST>(lds_dst, v);                  // 8-bit: widen to 16-bit
+    }
+}
+
+template <typename ST, int OUTB, int HW>
+__global__ __launch_bounds__(kThreads) void strip_kernel(const ScaleArgs a) {
+    extern __shared__ __align__(16) uint16_t lds[];
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int frame = L / a.tiles;
+    int t = L - frame * a.tiles;
+    int p = 0;
+    if (a.nplanes > 1 && t >= a.pl[1].tile_base) p = 1;
+    if (a.nplanes > 2 && t >= a.pl[2].tile_base) p = 2;
+    const PlaneJob &J = a.pl[p];
+    t -= J.tile_base;
+    const int seg = t / J.tiles_x, tx = t - seg * J.tiles_x;
+    const int x0 = tx * kTileW, nx = min(kTileW, J.dw - x0);
+    const int c0 = J.tile_c0[tx], cn = J.tile_cn[tx];
+    const int S = J.S;
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int cx = lane * 4;
+    uint16_t *src_t = lds;                                                  // [maxnew][S]
+    uint32_t *win = reinterpret_cast<uint32_t *>(lds + J.maxnew * S);       // [ring/2][256] row pairs
+    const ST *sbase = reinterpret_cast<const ST *>(a.src[p] + frame * a.sfs[p]);
+    uint8_t *dbase = a.dst[p] + frame * a.dfs[p];
+
+    // ---- horizontal taps of this lane's 4 columns over its HW-dword window ----
+    constexpr int hshift = sizeof(ST) == 1 ? 7 : 9;
+    const int g = tx * 64 + lane;
+    const int hb = J.hbase4[g];
+    v2i16 hc[4][HW];
+    {
+        const int4 *hp4 = reinterpret_cast<const int4 *>(J.hcoefw + (int64_t)g * 4 * HW);
+#pragma unroll
+        for (int i = 0; i < HW; ++i) {
+            const int4 v = hp4[i];
+            const int e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) hc[(4 * i + q) / HW][(4 * i + q) % HW] = __builtin_bit_cast(v2i16, e[q]);
+        }
+    }
+
+    // ---- staging (16-B loads through the plane's buffer resource) ----------
+    constexpr int CH = 16 / sizeof(ST);
+    const int cpr = (cn + CH - 1) / CH;  // 16-B chunks per staged row (<= kThreads, host-checked)
+    const int64_t sls = a.sls[p];
+    const int sw = J.sw;
+    const int64_t last_row = std::min<int64_t>(sls, ((int64_t)sw * sizeof(ST) + 15) & ~int64_t(15));
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(sbase, (int)((int64_t)(J.sh - 1) * sls + last_row));
+    const int cbyte = c0 * (int)sizeof(ST);
+    const int s_rstep = kThreads / cpr;
+    const int s_r0 = tid / cpr, s_ch = tid - s_r0 * cpr;
+    const bool s_on = s_r0 < s_rstep;
+    const int s_lds = s_r0 * S + s_ch * CH;
+    const int s_goff = s_r0 * (int)sls + cbyte + s_ch * 16;
+    auto prefetch = [&](Prefetch<ST> &pf, int from, int hi_) {
+        const int nrow = hi_ - from;
+#pragma unroll
+        for (int k = 0; k < kPF; ++k) {
+            const int r = s_r0 + k * s_rstep;
+            pf.v[k] = bload16(rs, (s_on && r < nrow) ? s_goff + (from + k * s_rstep) * (int)sls : kOobOff);
+        }
+    };
+    auto commit = [&](const Prefetch<ST> &pf, int from, int hi_) {
+        const int nrow = hi_ - from;
+        if (!s_on) return;
+#pragma unroll
+        for (int k = 0; k < kPF; ++k)
+            if (s_r0 + k * s_rstep < nrow) store_raw16<ST>(src_t + s_lds + k * s_rstep * S, pf.v[k]);
+        for (int k = kPF; s_r0 + k * s_rstep < nrow; ++k)
+            store_raw16<ST>(src_t + s_lds + k * s_rstep * S, bload16(rs, s_goff + (from + k * s_rstep) * (int)sls));
+    };
+
+    // 4 outputs of one staged row (15-bit intermediates, hScale*To15 clip)
+    auto hrow4 = [&](const uint16_t *row, int out[4]) {
+        const uint16_t *sp = row + hb;
+        uint32_t w[HW];
+#pragma unroll
+        for (int d = 0; d + 1 < HW; d += 2) {
+            const uint2 v = *reinterpret_cast<const uint2 *>(sp + 2 * d);
+            w[d] = v.x;
+            w[d + 1] = v.y;
+        }
+        if constexpr (HW & 1) w[HW - 1] = *reinterpret_cast<const uint32_t *>(sp + 2 * (HW - 1));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            int acc = dot2_first(__builtin_bit_cast(v2i16, w[0]), hc[j][0]);
+#pragma unroll
+            for (int d = 1; d < HW; ++d) acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, w[d]), hc[j][d], acc, false);
+            acc >>= hshift;
+            out[j] = acc < 32767 ? acc : 32767;
+        }
+    };
+
+    const int y_begin = seg * J.seg_h, y_end = min(J.dh, y_begin + J.seg_h);
+    const int cho = J.cho;
+    int next_src = J.chunk_lo[y_begin / cho];
+    int base = next_src & ~1;
+    Prefetch<ST> pf;
+    prefetch(pf, next_src, J.chunk_hi[y_begin / cho]);
+    const bool lane_any = cx < nx, lane_full = cx + 4 <= nx;
+    const int xo = x0 + cx;
+    const int64_t dls = a.dls[p];
+    const int vtp = J.vtp;
+    const kconst int32_t *vrow = as_kconst<int32_t>(J.vrow16);
+    for (int y0 = y_begin; y0 < y_end; y0 += cho) {
+        const int ci = y0 / cho;
+        const int lo = J.chunk_lo[ci], hi = J.chunk_hi[ci];
+        if (next_src < lo) next_src = lo;
+        const int nnew = hi - next_src;
+        const int nbase = lo & ~1;
+        const int keep = next_src > nbase ? (next_src - nbase + 1) >> 1 : 0;
+        const int shift = (nbase - base) >> 1;
+        // kept pairs: read now (other waves may still read them in the previous
+        // V pass), written down after the barrier
+        const bool keep_regs = keep <= 4 * kKeepRegs;
+        uint4 kp0 = {0, 0, 0, 0}, kp1 = {0, 0, 0, 0};  // pairs wave and wave + 4
+        if (shift > 0 && keep_regs) {
+            const int top = (J.ring >> 1) - 1;  // unconditional reads, clamped into the window
+            kp0 = *reinterpret_cast<const uint4 *>(win + min(wave + shift, top) * kTileW + cx);
+            kp1 = *reinterpret_cast<const uint4 *>(win + min(wave + 4 + shift, top) * kTileW + cx);
+        }
+        if (nnew > 0) commit(pf, next_src, hi);
+        __syncthreads();  // staged rows visible; every wave has left the previous V pass
+        const int after = nnew > 0 ? hi : next_src;
+        if (y0 + cho < y_end) prefetch(pf, max(after, J.chunk_lo[ci + 1]), J.chunk_hi[ci + 1]);
+        if (shift > 0) {
+            if (keep_regs) {
+                if (wave < keep) *reinterpret_cast<uint4 *>(win + wave * kTileW + cx) = kp0;
+                if (wave + 4 < keep) *reinterpret_cast<uint4 *>(win + (wave + 4) * kTileW + cx) = kp1;
+            } else {  // long windows (large downscales): column-sequential move
+                for (int k = 0; k < keep; ++k) win[k * kTileW + tid] = win[(k + shift) * kTileW + tid];
+                __syncthreads();
+            }
+        }
+        base = nbase;
+        // ---- horizontal pass: row pairs of the window, wave-strided ----------
+        if (nnew > 0) {
+            const int i0 = next_src - base;
+            const int kf0 = (i0 + 1) >> 1, kf1 = (i0 + nnew) >> 1;
+            if ((i0 & 1) && wave == ((i0 >> 1) & 3)) {  // high row of a kept pair (same wave moved it)
+                int o[4];
+                hrow4(src_t, o);
+                uint16_t *w16 = reinterpret_cast<uint16_t *>(win + (i0 >> 1) * kTileW + cx);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) w16[2 * j + 1] = static_cast<uint16_t>(o[j]);
+            }
+            if (((i0 + nnew) & 1) && wave == (kf1 & 3)) {  // low row of the last pair
+                int o[4];
+                hrow4(src_t + (nnew - 1) * S, o);
+                uint4 v;
+                v.x = o[0] & 0xffff; v.y = o[1] & 0xffff; v.z = o[2] & 0xffff; v.w = o[3] & 0xffff;
+                *reinterpret_cast<uint4 *>(win + kf1 * kTileW + cx) = v;
+            }
+            for (int k = kf0 + wave; k < kf1; k += 4) {
+                const int ra = 2 * k - i0;
+                int oa[4], ob[4];
+                hrow4(src_t + ra * S, oa);
+                hrow4(src_t + (ra + 1) * S, ob);
+                uint4 v;
+                v.x = __builtin_amdgcn_perm(ob[0], oa[0], 0x05040100u);
+                v.y = __builtin_amdgcn_perm(ob[1], oa[1], 0x05040100u);
+                v.z = __builtin_amdgcn_perm(ob[2], oa[2], 0x05040100u);
+                v.w = __builtin_amdgcn_perm(ob[3], oa[3], 0x05040100u);
+                *reinterpret_cast<uint4 *>(win + k * kTileW + cx) = v;
+            }
+            next_src = hi;
+        }
+        __syncthreads();  // window complete
+        // ---- vertical pass: one output row per wave --------------------------
+        const int ny = min(cho, y_end - y0);
+        // VT (= vtp) tap pairs, compile-time per instance: every window read of
+        // a row is in flight before the first v_dot2 waits on one
+        auto vpass = [&](auto vt_c) {
+            constexpr int VT = decltype(vt_c)::value;
+            for (int yy = wave; yy < ny; yy += 4) {
+                const int y = y0 + yy;
+                // row tables through the scalar (constant) cache: SGPR operands
+                const kconst int32_t *row = vrow + (int64_t)y * 16;  // one s_load_dwordx16
+                const int vb = (row[0] - nbase) >> 1;
+                const kconst int32_t *cp = row + 1;
+                const uint4 *rp = reinterpret_cast<const uint4 *>(win + vb * kTileW + cx);
+                uint4 q[VT];
+#pragma unroll
+                for (int j = 0; j < VT; ++j) q[j] = rp[j * (kTileW / 4)];
+                int acc[4];
+                if constexpr (OUTB == 8) {
+                    const int drow = y & 7;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[j] = (a.dither ? c_dither[drow][(xo + j + J.dither_off) & 7] : 64) << 12;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[j] = 1 << (10 + 16 - OUTB);
+                }
+#pragma unroll
+                for (int j = 0; j < VT; ++j) {
+                    const v2i16 c2 = __builtin_bit_cast(v2i16, cp[j]);
+                    acc[0] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].x), c2, acc[0], false);
+                    acc[1] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].y), c2, acc[1], false);
+                    acc[2] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].z), c2, acc[2], false);
+                    acc[3] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].w), c2, acc[3], false);
+                }
+                if (!lane_any) continue;
+                constexpr int sh = OUTB == 8 ? 19 : 11 + 16 - OUTB;
+                constexpr int mx = (1 << OUTB) - 1;
+                int o[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[j] = min(max(acc[j] >> sh, 0), mx);
+                uint8_t *drow_p = dbase + (int64_t)y * dls;
+                if constexpr (OUTB == 8) {
+                    if (lane_full && a.vec_dst) {
+                        *reinterpret_cast<uint32_t *>(drow_p + xo) =
+                            (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | ((uint32_t)o[3] << 24);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (xo + j < J.dw) drow_p[xo + j] = (uint8_t)o[j];
+                    }
+                } else {
+                    uint16_t *d16 = reinterpret_cast<uint16_t *>(drow_p);
+                    if (lane_full && a.vec_dst) {
+                        uint2 v;
+                        v.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+                        v.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+                        *reinterpret_cast<uint2 *>(d16 + xo) = v;
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (xo + j < J.dw) d16[xo + j] = (uint16_t)o[j];
+                    }
+                }
+            }
+        };
+        switch (vtp) {  // uniform, once per chunk
+        case 1: vpass(std::integral_constant<int, 1>{}); break;
+        case 2: vpass(std::integral_constant<int, 2>{}); break;
+        case 3: vpass(std::integral_constant<int, 3>{}); break;
+        case 4: vpass(std::integral_constant<int, 4>{}); break;
+        case 5: vpass(std::integral_constant<int, 5>{}); break;
+        case 6: vpass(std::integral_constant<int, 6>{}); break;
+        case 7: vpass(std::integral_constant<int, 7>{}); break;
+        default: vpass(std::integral_constant<int, 8>{}); break;
+        }
+    }
+}
+
 // planarCopyWrapper (same subsampling, same or wider depth): 8 samples per lane.
 __global__ __launch_bounds__(256) void copy_widen_kernel(const uint8_t *src, int64_t sls, int64_t sfs, int sbytes,
                                                          uint8_t *dst, int64_t dls, int64_t dfs, int dbytes,
@@ -503,6 +799,21 @@ KernelFn pick_ht_tw(int ht) {
 }
 
 template <typename ST, int OUTB>
+KernelFn pick_strip(int hw) {
+    switch (hw) {
+    case 3: return strip_kernel<ST, OUTB, 3>;
+    case 4: return strip_kernel<ST, OUTB, 4>;
+    case 5: return strip_kernel<ST, OUTB, 5>;
+    case 6: return strip_kernel<ST, OUTB, 6>;
+    case 8: return strip_kernel<ST, OUTB, 8>;
+    case 10: return strip_kernel<ST, OUTB, 10>;
+    case 12: return strip_kernel<ST, OUTB, 12>;
+    case 16: return strip_kernel<ST, OUTB, 16>;
+    default: return nullptr;
+    }
+}
+
+template <typename ST, int OUTB>
 KernelFn pick_ht(int ht, bool tw256) {
     return tw256 ? pick_ht_tw<ST, OUTB, kTileW>(ht) : pick_ht_tw<ST, OUTB, 0>(ht);
 }
@@ -530,6 +841,9 @@ struct pp_scale_plan {
     void *scratch = nullptr; int64_t scratch_plane[3] = {0, 0, 0}; // GENERIC_UYVY planar 4:2:2 temp
     int scratch_frames = 0;
     size_t lds_bytes = 0;
+    pp::PlaneJob fjob[3]{}; // strip_kernel jobs (fast_hw > 0)
+    int fast_hw = 0;        // H window dwords of strip_kernel, 0 = generic kernel only
+    size_t fast_lds = 0;
 };
 
 namespace {
@@ -542,6 +856,9 @@ struct HostPlane {
     std::vector<int32_t> vbase, vcoef2;  // V window as even-aligned row pairs
     int vtp = 1;
     int tiles_x = 0, nseg = 0, tw = 0, seg_h = 0, cho = 0, ring = 0, maxnew = 0, S = 0;
+    // strip_kernel layout
+    std::vector<int32_t> hbase4, hcoefw, vrow16;
+    int hw_need = 0, max_base = 0, S_fast = 0;
 };
 
 // Vertical taps regrouped as row pairs starting at an even row (the ring keeps
@@ -663,6 +980,68 @@ int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::
     return -1;
 }
 
+// strip_kernel windows: per 4-column lane group, an 8-B aligned base in the
+// staged row and the dwords that hold every non-zero tap of its 4 outputs.
+void fast_windows(HostPlane &hp, int dw) {
+    const int taps = hp.h.taps;
+    hp.hbase4.assign((size_t)hp.tiles_x * 64, 0);
+    hp.hw_need = 1;
+    hp.max_base = 0;
+    for (int tx = 0; tx < hp.tiles_x; ++tx)
+        for (int g = 0; g < 64; ++g) {
+            int lo = INT32_MAX, end = 0;
+            for (int j = 0; j < 4; ++j) {
+                const int x = tx * pp::kTileW + 4 * g + j;
+                if (x >= dw) break;
+                const int16_t *c = &hp.h.coef[(size_t)x * taps];
+                for (int k = 0; k < taps; ++k)
+                    if (c[k]) {
+                        lo = std::min(lo, hp.h.pos[x] + k);
+                        end = std::max(end, hp.h.pos[x] + k + 1);
+                    }
+            }
+            if (lo == INT32_MAX) continue;
+            const int base = (lo - hp.c0[tx]) & ~3;
+            hp.hbase4[(size_t)tx * 64 + g] = base;
+            hp.hw_need = std::max(hp.hw_need, (end - hp.c0[tx] - base + 1) / 2);
+            hp.max_base = std::max(hp.max_base, base);
+        }
+}
+
+// Taps of every output re-laid over its lane group's HW dwords (zero elsewhere).
+void fast_coefs(HostPlane &hp, int dw, int HW) {
+    const int taps = hp.h.taps;
+    hp.hcoefw.assign((size_t)hp.tiles_x * 64 * 4 * HW, 0);
+    uint16_t *h16 = reinterpret_cast<uint16_t *>(hp.hcoefw.data());
+    for (int tx = 0; tx < hp.tiles_x; ++tx)
+        for (int g = 0; g < 64; ++g)
+            for (int j = 0; j < 4; ++j) {
+                const int x = tx * pp::kTileW + 4 * g + j;
+                if (x >= dw) break;
+                const int base = hp.hbase4[(size_t)tx * 64 + g];
+                for (int k = 0; k < taps; ++k) {
+                    const int16_t c = hp.h.coef[(size_t)x * taps + k];
+                    if (!c) continue;
+                    const int s = hp.h.pos[x] + k - hp.c0[tx] - base;  // in [0, 2*HW)
+                    h16[(((size_t)tx * 64 + g) * 4 + j) * HW * 2 + s] = (uint16_t)c;
+                }
+            }
+    // per output row: window base row, then the V tap pairs padded to 8
+    const int n = (int)hp.vbase.size();
+    hp.vrow16.assign((size_t)n * 16, 0);
+    for (int i = 0; i < n; ++i) {
+        hp.vrow16[(size_t)i * 16] = hp.vbase[i];
+        for (int j = 0; j < hp.vtp; ++j) hp.vrow16[(size_t)i * 16 + 1 + j] = hp.vcoef2[(size_t)i * hp.vtp + j];
+    }
+}
+
+inline int hw_bucket(int need) {
+    static const int b[] = {3, 4, 5, 6, 8, 10, 12, 16};
+    for (int v : b)
+        if (need <= v) return v;
+    return -1;
+}
+
 }  // namespace
 
 extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, int dw, int dh,
@@ -732,6 +1111,32 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
         if (plan_tiles(hp[c], src_w, src_h, dst_w, dst_h, &P->lds_bytes, &err))
             PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
     }
+    // strip_kernel eligibility: 256-column strips, <= 8 V tap pairs, one H window
+    // bucket for both planes, single-pass staging, LDS within the budget
+    {
+        const char *force = std::getenv("PIXPATH_SCALE_KERNEL");
+        bool ok = !(force && std::strcmp(force, "generic") == 0);
+        const int CH = si.depth > 8 ? 8 : 16;
+        int need = 1;
+        for (int c = 0; c < 2 && ok; ++c) {
+            ok = hp[c].tw == kTileW && hp[c].vtp <= 8;
+            for (int v : hp[c].cn) ok = ok && (v + CH - 1) / CH <= kThreads;
+            if (!ok) break;
+            fast_windows(hp[c], c ? P->cdw : dw);
+            need = std::max(need, hp[c].hw_need);
+        }
+        const int HW = ok ? hw_bucket(need) : -1;
+        size_t lds = 0;
+        for (int c = 0; c < 2 && HW > 0; ++c) {
+            fast_coefs(hp[c], c ? P->cdw : dw, HW);
+            hp[c].S_fast = std::max(hp[c].S, (hp[c].max_base + 2 * HW + 15) & ~15);
+            lds = std::max(lds, (size_t)hp[c].maxnew * hp[c].S_fast * 2 + (size_t)hp[c].ring * kTileW * 2);
+        }
+        if (HW > 0 && lds <= (size_t)kLdsBudget) {
+            P->fast_hw = HW;
+            P->fast_lds = lds;
+        }
+    }
 
     if (!ctx) {
         *out = P.release();
@@ -743,12 +1148,13 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
     size_t total = 0;
     for (int c = 0; c < 2; ++c)
         total += sz4(hp[c].h.pos.size()) + sz2(hp[c].h.coef.size()) + sz4(hp[c].vbase.size()) +
-                 sz4(hp[c].vcoef2.size()) + 2 * sz4(hp[c].c0.size()) + 2 * sz4(hp[c].lo.size());
+                 sz4(hp[c].vcoef2.size()) + 2 * sz4(hp[c].c0.size()) + 2 * sz4(hp[c].lo.size()) +
+                 sz4(hp[c].hbase4.size()) + sz4(hp[c].hcoefw.size()) + sz4(hp[c].vrow16.size());
     PP_HIP(hipSetDevice(ctx->device));
     PP_HIP(hipMalloc(&P->dev, total));
     std::vector<uint8_t> host(total, 0);
     size_t off = 0;
-    const int32_t *dptr32[2][7];
+    const int32_t *dptr32[2][10] = {};
     const int16_t *dptr16[2][1];
     auto put = [&](const void *src, size_t bytes, size_t padded) {
         std::memcpy(host.data() + off, src, bytes);
@@ -765,6 +1171,11 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
         dptr32[c][3] = (const int32_t *)put(hp[c].cn.data(), hp[c].cn.size() * 4, sz4(hp[c].cn.size()));
         dptr32[c][4] = (const int32_t *)put(hp[c].lo.data(), hp[c].lo.size() * 4, sz4(hp[c].lo.size()));
         dptr32[c][5] = (const int32_t *)put(hp[c].hi.data(), hp[c].hi.size() * 4, sz4(hp[c].hi.size()));
+        if (P->fast_hw) {
+            dptr32[c][7] = (const int32_t *)put(hp[c].hbase4.data(), hp[c].hbase4.size() * 4, sz4(hp[c].hbase4.size()));
+            dptr32[c][8] = (const int32_t *)put(hp[c].hcoefw.data(), hp[c].hcoefw.size() * 4, sz4(hp[c].hcoefw.size()));
+            dptr32[c][9] = (const int32_t *)put(hp[c].vrow16.data(), hp[c].vrow16.size() * 4, sz4(hp[c].vrow16.size()));
+        }
     }
     PP_HIP(hipMemcpy(P->dev, host.data(), total, hipMemcpyHostToDevice));
 
@@ -786,6 +1197,9 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
         J.vbase = dptr32[c][1]; J.vcoef2 = dptr32[c][6];
         J.tile_c0 = dptr32[c][2]; J.tile_cn = dptr32[c][3];
         J.chunk_lo = dptr32[c][4]; J.chunk_hi = dptr32[c][5];
+        J.hbase4 = dptr32[c][7]; J.hcoefw = dptr32[c][8]; J.vrow16 = dptr32[c][9];
+        P->fjob[p] = J;
+        P->fjob[p].S = hp[c].S_fast;
     }
     *out = P.release();
     return PP_OK;
@@ -797,6 +1211,11 @@ extern "C" int pp_scale_plan_destroy(pp_scale_plan *P) {
     if (P->scratch) (void)hipFree(P->scratch);
     delete P;
     return PP_OK;
+}
+
+extern "C" int pp_scale_plan_path(const pp_scale_plan *P) {
+    if (!P) PP_FAIL(PP_ERR_INVALID, "null plan");
+    return (P->kind == pp_scale_plan::GENERIC || P->kind == pp_scale_plan::GENERIC_UYVY) ? P->fast_hw : 0;
 }
 
 extern "C" int pp_scale_plan_filter(const pp_scale_plan *P, int which, int16_t *coef, int32_t *pos, int capacity) {
@@ -839,10 +1258,19 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
     }
     const bool tw256 = P->job[0].tw == kTileW && P->job[1].tw == kTileW && P->job[2].tw == kTileW;
     KernelFn k;
-    if (P->si.depth == 8)
+    size_t lds = P->lds_bytes;
+    if (P->fast_hw && a.vec_src) {
+        for (int p = 0; p < 3; ++p) a.pl[p] = P->fjob[p];
+        lds = P->fast_lds;
+        if (P->si.depth == 8)
+            k = out_depth == 8 ? pick_strip<uint8_t, 8>(P->fast_hw) : pick_strip<uint8_t, 10>(P->fast_hw);
+        else
+            k = out_depth == 8 ? pick_strip<uint16_t, 8>(P->fast_hw) : pick_strip<uint16_t, 10>(P->fast_hw);
+    } else if (P->si.depth == 8) {
         k = out_depth == 8 ? pick_ht<uint8_t, 8>(P->ht, tw256) : pick_ht<uint8_t, 10>(P->ht, tw256);
-    else
+    } else {
         k = out_depth == 8 ? pick_ht<uint16_t, 8>(P->ht, tw256) : pick_ht<uint16_t, 10>(P->ht, tw256);
+    }
     if (!k) PP_FAIL(PP_ERR_UNSUPPORTED, "no kernel for %d taps", P->ht);
     const int tiles = P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y;
     a.tiles = tiles;
@@ -854,7 +1282,7 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
             b.src[p] += f0 * a.sfs[p];
             b.dst[p] += f0 * a.dfs[p];
         }
-        hipLaunchKernelGGL(k, dim3(tiles * nf), dim3(kThreads), P->lds_bytes, st, b);
+        hipLaunchKernelGGL(k, dim3(tiles * nf), dim3(kThreads), lds, st, b);
     }
     PP_HIP(hipGetLastError());
     return PP_OK;

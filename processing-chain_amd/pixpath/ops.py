@@ -81,6 +81,11 @@ class Scaler:
                 pass
             self.handle = None
 
+    @property
+    def kernel_path(self):
+        """> 0: the strip kernel runs (its H window in dwords); 0: the general kernel."""
+        return check(lib().pp_scale_plan_path(self.handle))
+
     def filter(self, which):
         """FFmpeg-layout filter (coef [n, size] int16, pos [n] int32) or None (unscaled path)."""
         n = [self.dw, -((-self.dw) >> (self.dst_fmt.hsub)), self.dh,

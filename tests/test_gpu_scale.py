@@ -48,15 +48,22 @@ def _frames(content, fmt, w, h, n, seed):
     return [synth.smooth_frame(t, fmt, w, h) for t in range(n)]
 
 
+@pytest.mark.parametrize("kernel", ["auto", "generic"])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "%dx%d_f%d->%dx%d_f%d_%x" % (c[1], c[2], c[0], c[4], c[5], c[3], c[6]))
-def test_scale_matches_oracle(gpu, case):
+def test_scale_matches_oracle(gpu, case, kernel, monkeypatch):
+    """Both scaler kernels (strip kernel where the plan allows it, and the
+    general kernel forced by PIXPATH_SCALE_KERNEL=generic) against the oracle."""
     from pixpath import ops
     from pixpath.frames import FrameBatch
     sf, sw, sh, df, dw, dh, flags, content = case
+    if kernel == "generic":
+        monkeypatch.setenv("PIXPATH_SCALE_KERNEL", "generic")
     n = 2
     frames = _frames(content, sf, sw, sh, n, seed=910)
     src = FrameBatch.from_numpy(sf, synth.batch(frames), device=gpu)
     sc = ops.Scaler(sf, sw, sh, df, dw, dh, flags=flags)
+    if kernel == "generic":
+        assert sc.kernel_path == 0
     out = sc(src).to_numpy()
     import torch
     torch.cuda.synchronize()
@@ -116,3 +123,14 @@ def test_scale_interleaved_unaligned_source(gpu, case):
         ref = po.scale(sf, frames[i], df, dw, dh, flags)
         for p, r in enumerate(ref):
             assert np.array_equal(out[p][i], r), "frame %d plane %d" % (i, p)
+
+
+def test_strip_kernel_selected_for_bench_shapes(gpu):
+    """The headline shapes run the strip kernel (config 2 lanczos/bicubic upscale,
+    config 3 downscales); the tiny and 6x cases fall back to the general kernel."""
+    from pixpath import ops
+    assert ops.Scaler(po.YUV422P10LE, 1280, 720, po.YUV422P10LE, 1920, 1080, flags="lanczos").kernel_path == 6
+    assert ops.Scaler(po.YUV422P10LE, 1280, 720, po.YUV422P10LE, 1920, 1080, flags="bicubic").kernel_path == 4
+    assert ops.Scaler(po.YUV422P10LE, 3840, 2160, po.YUV422P10LE, 1920, 1080).kernel_path == 8
+    assert ops.Scaler(po.YUV420P, 3840, 2160, po.YUV422P10LE, 1920, 1080).kernel_path == 8
+    assert ops.Scaler(po.YUV420P, 8, 8, po.YUV420P, 3, 3).kernel_path == 0
