@@ -503,7 +503,9 @@ __global__ __launch_bounds__(kThreads) void strip_kernel(const ScaleArgs a) {
     t -= J.tile_base;
     const int seg = t / J.tiles_x, tx = t - seg * J.tiles_x;
     const int x0 = tx * kTileW, nx = min(kTileW, J.dw - x0);
-    const int c0 = J.tile_c0[tx], cn = J.tile_cn[tx];
+    const int c0 = as_kconst<int32_t>(J.tile_c0)[tx], cn = as_kconst<int32_t>(J.tile_cn)[tx];
+    // chunk tables through the scalar cache: no vector-memory wait at chunk starts
+    const kconst int32_t *chunk_lo = as_kconst<int32_t>(J.chunk_lo), *chunk_hi = as_kconst<int32_t>(J.chunk_hi);
     const int S = J.S;
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -528,6 +530,13 @@ __global__ __launch_bounds__(kThreads) void strip_kernel(const ScaleArgs a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) hc[(4 * i + q) / HW][(4 * i + q) % HW] = __builtin_bit_cast(v2i16, e[q]);
         }
+        // consume the taps here, so their vmcnt wait is placed before the chunk
+        // loop (inside it, the wait would also cover the previous chunk's stores)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int d = 0; d < HW; ++d) asm volatile("" ::"v"(hc[j][d]));
+        asm volatile("" ::"v"(hb));
     }
 
     // ---- staging (16-B loads through the plane's buffer resource) ----------
@@ -584,10 +593,10 @@ __global__ __launch_bounds__(kThreads) void strip_kernel(const ScaleArgs a) {
 
     const int y_begin = seg * J.seg_h, y_end = min(J.dh, y_begin + J.seg_h);
     const int cho = J.cho;
-    int next_src = J.chunk_lo[y_begin / cho];
+    int next_src = chunk_lo[y_begin / cho];
     int base = next_src & ~1;
     Prefetch<ST> pf;
-    prefetch(pf, next_src, J.chunk_hi[y_begin / cho]);
+    prefetch(pf, next_src, chunk_hi[y_begin / cho]);
     const bool lane_any = cx < nx, lane_full = cx + 4 <= nx;
     const int xo = x0 + cx;
     const int64_t dls = a.dls[p];
@@ -595,7 +604,7 @@ __global__ __launch_bounds__(kThreads) void strip_kernel(const ScaleArgs a) {
     const kconst int32_t *vrow = as_kconst<int32_t>(J.vrow16);
     for (int y0 = y_begin; y0 < y_end; y0 += cho) {
         const int ci = y0 / cho;
-        const int lo = J.chunk_lo[ci], hi = J.chunk_hi[ci];
+        const int lo = chunk_lo[ci], hi = chunk_hi[ci];
         if (next_src < lo) next_src = lo;
         const int nnew = hi - next_src;
         const int nbase = lo & ~1;
@@ -613,7 +622,7 @@ __global__ __launch_bounds__(kThreads) void strip_kernel(const ScaleArgs a) {
         if (nnew > 0) commit(pf, next_src, hi);
         __syncthreads();  // staged rows visible; every wave has left the previous V pass
         const int after = nnew > 0 ? hi : next_src;
-        if (y0 + cho < y_end) prefetch(pf, max(after, J.chunk_lo[ci + 1]), J.chunk_hi[ci + 1]);
+        if (y0 + cho < y_end) prefetch(pf, max(after, chunk_lo[ci + 1]), chunk_hi[ci + 1]);
         if (shift > 0) {
             if (keep_regs) {
                 if (wave < keep) *reinterpret_cast<uint4 *>(win + wave * kTileW + cx) = kp0;
@@ -663,10 +672,11 @@ __global__ __launch_bounds__(kThreads) void strip_kernel(const ScaleArgs a) {
         // a row is in flight before the first v_dot2 waits on one
         auto vpass = [&](auto vt_c) {
             constexpr int VT = decltype(vt_c)::value;
-            for (int yy = wave; yy < ny; yy += 4) {
+            const kconst int32_t *row = vrow + (int64_t)(y0 + wave) * 16;
+            uint8_t *drow_p = dbase + (int64_t)(y0 + wave) * dls;
+            for (int yy = wave; yy < ny; yy += 4, row += 64, drow_p += 4 * dls) {
                 const int y = y0 + yy;
                 // row tables through the scalar (constant) cache: SGPR operands
-                const kconst int32_t *row = vrow + (int64_t)y * 16;  // one s_load_dwordx16
                 const int vb = (row[0] - nbase) >> 1;
                 const kconst int32_t *cp = row + 1;
                 const uint4 *rp = reinterpret_cast<const uint4 *>(win + vb * kTileW + cx);
@@ -697,7 +707,6 @@ __global__ __launch_bounds__(kThreads) void strip_kernel(const ScaleArgs a) {
                 int o[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) o[j] = min(max(acc[j] >> sh, 0), mx);
-                uint8_t *drow_p = dbase + (int64_t)y * dls;
                 if constexpr (OUTB == 8) {
                     if (lane_full && a.vec_dst) {
                         *reinterpret_cast<uint32_t *>(drow_p + xo) =
