@@ -162,7 +162,7 @@ def main():
         if os.path.exists(PMC_FILE):
             try:
                 pm = json.load(open(PMC_FILE))
-                k = pm.get("kernels", {}).get("scale_kernel")
+                k = pm.get("kernels", {}).get("strip_kernel") or pm.get("kernels", {}).get("scale_kernel")
                 if k and pm.get("frames_per_launch") == n:
                     traffic = k["hbm_bytes_per_launch"]
             except Exception:
@@ -191,7 +191,7 @@ def main():
             "siti_achieved_gbs": round(SITI_BYTES_PER_FRAME * n / (siti_ms / 1000.0) / 1e9, 1),
             "roofline": {
                 "bound": "hbm",
-                "kernel": "scale_kernel (fused H+V polyphase, one launch per 600-frame batch)",
+                "kernel": "strip_kernel (fused H+V polyphase over 256-column strips, one launch per 600-frame batch)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -14,7 +14,7 @@ import collections
 import json
 import sys
 
-KERNELS = {"scale_kernel": "pp::scale_kernel", "siti_kernel": "pp::siti_kernel", "v210_kernel": "pp::v210_kernel",
+KERNELS = {"scale_kernel": "pp::scale_kernel", "strip_kernel": "pp::strip_kernel", "siti_kernel": "pp::siti_kernel", "v210_kernel": "pp::v210_kernel",
            "pad_kernel": "pp::pad_kernel", "stall_kernel": "pp::stall_kernel", "cpvs_kernel": "pp::cpvs_kernel"}
 
 
