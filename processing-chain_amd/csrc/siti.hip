@@ -14,13 +14,13 @@
 // the band, so every pixel of the band is read from HBM once per frame; the
 // previous frame's band (TI) stays in registers (16 rows x 8 px packed in 64
 // VGPRs), only the two halo rows are read twice.
-// Precision: |G| = sqrt in fp32 and per-row (mean, M2) in fp32 -- std is
-// shift-invariant, so a relative rounding of ~1e-7 per sample moves SI by
-// ~1e-7 relative, well inside the 1e-4 tolerance -- merged across rows, lanes
+// Precision: |G| = sqrt in fp32; per lane and frame the shifted sums
+// S1 = sum(|G| - K), S2 = sum(|G| - K)^2 in fp32, K being one of the lane's own
+// samples of that frame (so S2 - S1^2/n cancels at most ~n eps, ~1e-5 relative,
+// and a constant-magnitude frame gives exactly 0), merged across lanes, waves
 // and bands in fp64 (Chan et al.).
-// Moments: SI keeps (count, mean, M2) of |G| -- per-row two-pass statistics
-// merged with Chan's parallel update, so a frame of constant gradient
-// magnitude gives exactly 0 (E[x^2]-mean^2 would cancel); TI keeps sum(d) and
+// Moments: SI keeps (count, mean, M2) of |G| per wave (from the lanes' shifted
+// sums, so no E[x^2]-mean^2 cancellation); TI keeps sum(d) and
 // sum(d^2) exact in 64-bit integers.  Per (frame, band) partials are written
 // without atomics and reduced in a fixed order by siti_finalize, so results
 // are bit-reproducible.
@@ -65,16 +65,6 @@ __device__ inline uint64_t wave_sum_u64(uint64_t v) {
     return v;
 }
 
-// Lane-local (n, mean, M2) in fp32, merged with Chan's update.
-__device__ inline void chan_merge_f(float &n, float &mean, float &m2, float nb, float meanb, float m2b) {
-    const float nn = n + nb;
-    const float delta = meanb - mean;
-    const float fb = nn > 0.f ? nb / nn : 0.f;
-    mean += delta * fb;
-    m2 += m2b + delta * delta * n * fb;
-    n = nn;
-}
-
 // One row of a lane's 8 pixels in load format: 4 dwords (u16) or 2 (u8).
 template <typename T>
 struct Row {
@@ -109,10 +99,12 @@ __device__ inline uint32_t pk_add(uint32_t a, uint32_t b) {
 __device__ inline uint32_t pk_sub(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2i16, a) - __builtin_bit_cast(v2i16, b));
 }
-// 2 * a + b per 16-bit half (v_pk_mad_u16; wraps like the int16 values it holds)
+// 2 * a + b per 16-bit half in one v_pk_mad_u16 (wraps like the int16 values it
+// holds; the compiler splits a * 2 + b into a shift and an add)
 __device__ inline uint32_t pk_2a_plus_b(uint32_t a, uint32_t b) {
-    const v2u16 two = {2, 2};
-    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u16, a) * two + __builtin_bit_cast(v2u16, b));
+    uint32_t r;
+    asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(0x00020002u), "v"(b));
+    return r;
 }
 // gx^2 + gy^2 of one (gx, gy) pair: the VOP3P form with an inline-constant
 // accumulator (the compiler's v_dot2c form needs a zeroed destination copy)
@@ -210,8 +202,13 @@ __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_
         vm[k] = v2f32{s0 ? 1.f : 0.f, s1 ? 1.f : 0.f};
         rc += s0 + s1;
     }
-    const float frc = static_cast<float>(rc);
-    const float inv_rc = rc ? 1.f / frc : 0.f;
+    // valid Sobel rows c of the band (the same for every frame) and whether
+    // the band's first window row (ri == 2, c = y0) is one of them
+    const int sobel_rows = max(0, min(y1 - 1, H - 2) - max(y0, 1) + 1);
+    const bool row2_valid = y0 >= 1 && y0 < y1 && y0 <= H - 2;
+    const double n_lane = static_cast<double>(rc) * sobel_rows;
+    // the lane's first valid Sobel column supplies the frame's shift K
+    const int kpick = halo ? 0 : max(0, min(kLanePx - 1, sobel_lo));
     const uint32_t ones = 0x00010001u;
 
     for (int f = f0; f < f1; ++f) {
@@ -219,7 +216,12 @@ __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_
         const bool nlive = f + 1 < f1;
         const uint8_t *nb = frames + (int64_t)(nlive ? f + 1 : f) * fs;
         const auto nrs = rsrc(nb);
-        float n_t = 0.f, mean_t = 0.f, m2_t = 0.f;
+        // shifted moments of |G|: x = |G| - K over the lane's valid columns,
+        // S1 = sum x, S2 = sum x^2 (K = one of the lane's own samples, so a
+        // constant-magnitude frame gives x = 0 exactly and SI = 0 exactly)
+        float K = 0.f;
+        v2f32 nkvm[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};  // -K * valid mask
+        v2f32 s1 = {0.f, 0.f}, s2 = {0.f, 0.f};
         int d1s = 0;        // |sum d| <= 16 rows * 8 px * 1023
         uint32_t d2s = 0;   // sum d^2 <= 16 * 8 * 1023^2 < 2^32
         uint32_t h1a[4], h2a[4], h1b[4], h2b[4];  // packed int16 pairs of the rows above
@@ -270,26 +272,21 @@ __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_
                     const int g0 = sq_norm(p0), g1 = sq_norm(p1);
                     mag[k] = v2f32{__fsqrt_rn(static_cast<float>(g0)), __fsqrt_rn(static_cast<float>(g1))};
                 }
-                // per-row two-pass statistics over the lane's valid columns (exact 0
-                // for a constant row), merged into the lane's running (n, mean, M2)
-                v2f32 sv = mag[0] * vm[0];
+                if (ri == 2 || (ri == 3 && !row2_valid)) {  // first valid Sobel row of the band
+                    float k = mag[0].x;
 #pragma unroll
-                for (int k = 1; k < 4; ++k) sv = pk_fma(mag[k], vm[k], sv);
-                const float rm = (sv.x + sv.y) * inv_rc;
-                const v2f32 nrm = {-rm, -rm};
-                v2f32 qv = {0.f, 0.f};
+                    for (int e = 1; e < kLanePx; ++e) k = kpick == e ? ((e & 1) ? mag[e >> 1].y : mag[e >> 1].x) : k;
+                    K = k;
+                    const v2f32 nk = {-K, -K};
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const v2f32 dv = (mag[k] + nrm) * vm[k];
-                    qv = pk_fma(dv, dv, qv);
+                    for (int j = 0; j < 4; ++j) nkvm[j] = vm[j] * nk;
                 }
-                const float rm2 = qv.x + qv.y;
-                const float nn = n_t + frc;
-                const float fb = frc * __builtin_amdgcn_rcpf(nn > 0.f ? nn : 1.f);
-                const float delta = rm - mean_t;
-                mean_t += delta * fb;
-                m2_t += rm2 + delta * delta * n_t * fb;
-                n_t = nn;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const v2f32 xv = pk_fma(mag[j], vm[j], nkvm[j]);  // (|G| - K) on valid columns, else 0
+                    s1 += xv;
+                    s2 = pk_fma(xv, xv, s2);
+                }
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -299,17 +296,20 @@ __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_
             // this row is consumed: start loading the next frame's row ri into it
             issue_row<T>(raw[ri], nrs, row_off(r, nlive));
         }
-        // wave reduction in fp64, fixed butterfly order: N, sum n*mean -> mean_w,
-        // then sum (M2 + n (mean - mean_w)^2); TI moments as integers
-        double cnt = n_t, sum = static_cast<double>(n_t) * static_cast<double>(mean_t);
+        // wave reduction in fp64, fixed butterfly order: N, sum (n K + S1) -> mean_w,
+        // then sum (x - mean_w)^2 = sum (S2 + 2 dK S1 + n dK^2), dK = K - mean_w;
+        // TI moments as integers
+        const double ls1 = static_cast<double>(s1.x) + static_cast<double>(s1.y);
+        const double ls2 = static_cast<double>(s2.x) + static_cast<double>(s2.y);
+        double cnt = n_lane, sum = n_lane * static_cast<double>(K) + ls1;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             cnt += __shfl_xor(cnt, o, 64);
             sum += __shfl_xor(sum, o, 64);
         }
         const double mean_w = cnt > 0.0 ? sum / cnt : 0.0;
-        const double dm = static_cast<double>(mean_t) - mean_w;
-        double m2 = static_cast<double>(m2_t) + static_cast<double>(n_t) * dm * dm;
+        const double dk = static_cast<double>(K) - mean_w;
+        double m2 = ls2 + 2.0 * dk * ls1 + n_lane * dk * dk;
         int64_t d1 = d1s;
         uint64_t d2 = d2s;
 #pragma unroll
