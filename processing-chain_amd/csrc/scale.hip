@@ -37,6 +37,8 @@ namespace pp {
 constexpr int kTileW = 256;      // widest output tile (columns); narrower for large downscales
 constexpr int kThreads = 256;    // 4 waves
 constexpr int kLdsBudget = 40 * 1024;
+constexpr int kChoMax = 32;     // output rows per chunk (upper bound)
+constexpr int kSegRows = 256;   // output rows per segment (target)
 
 __constant__ uint8_t c_dither[8][8] = {
     {36, 68, 60, 92, 34, 66, 58, 90},  {100, 4, 124, 28, 98, 2, 122, 26},
@@ -960,16 +962,27 @@ void row_chunks(HostPlane &hp, int sh, int dh, int cho, int seg_h, int *maxnew, 
     *ring = (wr + 1) & ~1;
 }
 
+// LDS budget per workgroup in bytes (PIXPATH_SCALE_LDS_KB overrides, measurement only)
+static size_t lds_budget() {
+    const char *e = std::getenv("PIXPATH_SCALE_LDS_KB");
+    return e ? (size_t)std::max(8, std::min(160, atoi(e))) * 1024 : (size_t)pp::kLdsBudget;
+}
+
 // Strip width / chunk height / segments for one plane: the widest strip and
 // tallest chunk whose LDS (staging + ring) fits the budget; ~256-row segments.
 int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::string *err) {
     static const int tws[] = {256, 128, 64, 32};
-    static const int chos[] = {32, 16, 8, 4, 2, 1};
+    static const int chos[] = {64, 32, 16, 8, 4, 2, 1};
+    // tuning overrides (measurement only): tallest chunk, rows per segment
+    const char *e_cho = std::getenv("PIXPATH_SCALE_CHO_MAX"), *e_seg = std::getenv("PIXPATH_SCALE_SEG_ROWS");
+    const int cho_max = e_cho ? std::max(1, atoi(e_cho)) : pp::kChoMax;
+    const int seg_rows = e_seg ? std::max(1, atoi(e_seg)) : pp::kSegRows;
     for (int tw : tws) {
         if (tw > 32 && tw / 2 >= dw) continue;  // narrower strips suffice for this plane
         const int S = col_windows(hp, sw, dw, tw);
         for (int cho : chos) {
-            int nseg = std::max(1, (dh + 128) / 256);
+            if (cho > cho_max) continue;
+            int nseg = std::max(1, (dh + seg_rows / 2) / seg_rows);
             int seg_h = (dh + nseg - 1) / nseg;
             seg_h = (seg_h + cho - 1) / cho * cho;
             nseg = (dh + seg_h - 1) / seg_h;
@@ -977,7 +990,7 @@ int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::
             row_chunks(hp, sh, dh, cho, seg_h, &maxnew, &ring);
             const size_t bytes = (size_t)maxnew * S * 2 + (size_t)ring * tw * 2 +
                                  (size_t)cho * hp.vtp * 4 + (size_t)cho * 4;
-            if (bytes > (size_t)pp::kLdsBudget) continue;
+            if (bytes > lds_budget()) continue;
             hp.tiles_x = (dw + tw - 1) / tw;
             hp.nseg = nseg; hp.tw = tw; hp.seg_h = seg_h; hp.cho = cho;
             hp.ring = ring; hp.maxnew = maxnew; hp.S = S;
@@ -1141,7 +1154,7 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
             hp[c].S_fast = std::max(hp[c].S, (hp[c].max_base + 2 * HW + 15) & ~15);
             lds = std::max(lds, (size_t)hp[c].maxnew * hp[c].S_fast * 2 + (size_t)hp[c].ring * kTileW * 2);
         }
-        if (HW > 0 && lds <= (size_t)kLdsBudget) {
+        if (HW > 0 && lds <= lds_budget()) {
             P->fast_hw = HW;
             P->fast_lds = lds;
         }
