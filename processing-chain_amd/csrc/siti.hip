@@ -136,18 +136,12 @@ __device__ inline void to_pairs(const Row<T> &r, uint32_t w[4]) {
 // branches around the loads.  The previous frame's band (TI) stays in
 // registers too, so every pixel is read from HBM once (plus the two halo rows).
 template <typename T>
-__global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_t ls, int64_t fs, int nframes,
-                                                   const uint8_t *prev, int W, int H, int tiles_x, int bands,
-                                                   int chunk, SitiPartial *part) {
+__device__ __forceinline__ void siti_range(const uint8_t *frames, int64_t ls, int64_t fs, int nframes,
+                                          const uint8_t *prev, int W, int H, int tiles_x, int tile, int f0, int f1,
+                                          SitiPartial *part) {
     constexpr int NR = kBand + 2;
-    // 1-D grid of frame chunks x tiles, XCD-aware: an XCD holds consecutive
-    // bands of one frame chunk, so the halo rows shared by adjacent bands hit its L2
-    const int ntiles = tiles_x * bands;
-    const int L = xcd_remap(blockIdx.x, gridDim.x);
-    const int ck = L / ntiles;
-    const int tile = L - ck * ntiles;  // tx + tiles_x * band
+    const int bands = (H + kBand - 1) / kBand;
     const int tx = tile % tiles_x, band = tile / tiles_x;
-    const int f0 = ck * chunk, f1 = min(nframes, f0 + chunk);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // lanes 1..62 own 8 pixels each; lanes 0 and 63 load the pixels just left
     // and right of the wave's span, so every neighbour comes from a shuffle
@@ -324,6 +318,29 @@ __global__ __launch_bounds__(256) void siti_kernel(const uint8_t *frames, int64_
     }
 }
 
+// 1-D grid sized to the resident workgroup slots; workgroup i walks the
+// (tile, frame) units [i*U/G, (i+1)*U/G) in tile-major order -- equal work per
+// workgroup (fixed frame chunks per band would leave slots idle whenever the
+// band count does not divide them) and at most one band switch per range.
+// XCD-aware: an XCD holds consecutive ranges, i.e. adjacent bands advancing
+// through the same frames together, so the halo rows they share hit its L2.
+template <typename T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void siti_kernel(const uint8_t *frames, int64_t ls, int64_t fs, int nframes,
+                                                   const uint8_t *prev, int W, int H, int tiles_x, int ntiles,
+                                                   SitiPartial *part) {
+    const int64_t total = (int64_t)ntiles * nframes;
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    int64_t u = total * L / gridDim.x;
+    const int64_t u1 = total * (L + 1) / gridDim.x;
+    while (u < u1) {
+        const int tile = (int)(u / nframes);
+        const int f0 = (int)(u - (int64_t)tile * nframes);
+        const int f1 = (int)min<int64_t>(nframes, f0 + (u1 - u));
+        siti_range<T>(frames, ls, fs, nframes, prev, W, H, tiles_x, tile, f0, f1, part);
+        u += f1 - f0;
+    }
+}
+
 // One workgroup per frame: each lane merges a strided subset of the partials,
 // then a fixed-shape LDS tree -- the order never depends on timing, so the
 // result is bit-reproducible.
@@ -378,18 +395,14 @@ extern "C" int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma
     const int bytes = bitdepth > 8 ? 2 : 1;
     const int tiles_x = (w + kSpan - 1) / kSpan, bands = (h + kBand - 1) / kBand;
     const int ntiles = tiles_x * bands;
-    // frames chunked per workgroup so that the grid is one wave of resident
-    // workgroups (a partial second wave would idle most of the chip); each chunk
-    // re-reads one previous-frame band for TI, so chunks stay long
+    // one wave of resident workgroups (a partial second wave would idle most of
+    // the chip), each walking an equal share of the (tile, frame) units
     int dev_cus = 0, per_cu = 0;
     PP_HIP(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     PP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, bytes == 2 ? (const void *)siti_kernel<uint16_t> : (const void *)siti_kernel<uint8_t>, 256, 0));
-    const int slots = std::max(1, dev_cus * std::max(1, per_cu));
-    int chunks = std::max(1, slots / ntiles);
-    if (chunks > nframes) chunks = nframes;
-    const int chunk = (nframes + chunks - 1) / chunks;
-    chunks = (nframes + chunk - 1) / chunk;
+    const int64_t slots = std::max(1, dev_cus * std::max(1, per_cu));
+    const int groups = (int)std::min<int64_t>(slots, (int64_t)ntiles * nframes);
     // The kernel reads each lane's 8 pixels as one 16-B (8-B) buffer load, so
     // rows must start on that granule; other layouts (odd widths packed
     // contiguously, views into a row) are first repacked on the device into a
@@ -423,9 +436,8 @@ extern "C" int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma
         PP_FAIL(PP_ERR_UNSUPPORTED, "frame of %lld bytes exceeds the 2 GiB buffer range", (long long)(h * ls));
     SitiPartial *part = nullptr;
     PP_HIP(hipMallocAsync((void **)&part, sizeof(SitiPartial) * (size_t)ntiles * 4 * nframes, st));
-    dim3 grid(ntiles * chunks);
     auto k = bytes == 2 ? siti_kernel<uint16_t> : siti_kernel<uint8_t>;
-    hipLaunchKernelGGL(k, grid, dim3(256), 0, st, src, ls, fs, nframes, psrc, w, h, tiles_x, bands, chunk, part);
+    hipLaunchKernelGGL(k, dim3(groups), dim3(256), 0, st, src, ls, fs, nframes, psrc, w, h, tiles_x, ntiles, part);
     hipLaunchKernelGGL(siti_finalize, dim3(nframes), dim3(256), 0, st, part, nframes, ntiles * 4, w, h,
                        prev != nullptr, si, ti);  // ntiles * 4 wave partials per frame
     PP_HIP(hipGetLastError());
