@@ -12,7 +12,7 @@ grep -E "^FAILED" gpurun_out/pytest_gpu_$TAG.log | head -20 || true
 # 0 = green, 1 = test failures: keep going; anything else (crash, abort, timeout) ends the call
 if [ $rc -gt 1 ]; then echo "stopping after pytest rc=$rc"; exit $rc; fi
 timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err && cat gpurun_out/bench_$TAG.json &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt_$TAG -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof_kt_$TAG.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt_$TAG -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof_kt_$TAG.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch_$TAG -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > gpurun_out/prof_fetch_$TAG.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_$TAG -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > gpurun_out/prof_write_$TAG.log 2>&1 &&
 python3 tools/pmc_traffic.py gpurun_out/prof_fetch_$TAG/run_counter_collection.csv gpurun_out/prof_write_$TAG/run_counter_collection.csv gpurun_out/prof_kt_$TAG/run_kernel_trace.csv gpurun_out/pmc_traffic_$TAG.json 600 > /dev/null &&
