@@ -1,21 +1,34 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X raw-frame pixel path (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1], "config 2"): one 10 s 1080p60 SRC ->
-  * P.910 SI/TI over 600 frames of 1920x1080 10-bit luma, and
-  * 600 frames of 1280x720 yuv422p10le upscaled (lanczos, swscale-exact) to a
-    1920x1080 yuv422p10le AVPVS.
-A step = one pass of that hot path over the 600-frame batch, inputs resident in
-HBM.  value = frames of that workload per second over all ranks (each frame
-gets both its SI/TI and its AVPVS upscale).  Multi-GPU: one process per GPU,
-each rank owns its own 600-frame PVS (PVS sharding, SURVEY.md section 8e, weak
-scaling); the only collectives are the timing barrier and the max-over-ranks
-of the elapsed time -- no data-path exchange.
+Unit of work = one PVS of BASELINE config 2: a 10 s 1080p60 SRC ->
+  * P.910 SI/TI over its 600 frames of 1920x1080 10-bit luma, and
+  * its 600 frames of 1280x720 yuv422p10le upscaled (lanczos, swscale-exact)
+    to a 1920x1080 yuv422p10le AVPVS.
+A step = every rank runs its share of a batch of PVSes (pixpath.batch.my_pvs,
+the reference's ParallelRunner unit, lib/cmd_utils.py:93-101), then the
+per-frame SI/TI of every PVS is gathered to rank 0 on the host (gloo).  Inputs
+are resident in HBM when the timed region starts.  Defaults: 32 PVS per rank
+(weak scaling), so 8 ranks run BASELINE config 5 (256 PVS = 153,600 frames);
+--pvs-total 256 runs config 5 at any rank count.
+value = frames of that workload per second over all ranks (each frame gets
+both its AVPVS upscale and its SI/TI).
 
-Extra fields: roofline of the dominant kernel (the fused scaler) from HIP
-events around its launches on the launch stream, the PMC traffic from a
-separate rocprofv3 --pmc pass (profiles/, see tools/pmc_traffic.py), and the
-CPU baseline (oracle/ C restatement, "port", bounded sample on host threads).
+Multi-GPU: one process per GPU.  Under `torch.distributed.run` the ranks come
+from its environment; `bench.py --gpus N` without it spawns the N ranks
+itself (pixpath.batch.spawn_local; the parent never touches the GPU).  The
+timing barrier, the max-over-ranks of the elapsed time and the SI/TI gather
+use a gloo group -- no RCCL, no device-side exchange.
+
+Extra fields: the roofline of the dominant kernel (strip_kernel) from HIP
+events around its launches on the launch stream, the PMC traffic of a
+separate rocprofv3 --pmc pass (profiles/pmc_traffic.json, tools/pmc_traffic.py),
+the PCIe-inclusive pipeline rate (pinned host buffers -> H2D -> kernels ->
+D2H, pixpath.pipeline, never `value`), and the CPU baseline (the oracle's C
+restatement, scale and SI/TI timed separately on host threads).
+
+Other workloads (profiles only, same schema): --workload config3-10 /
+config3-8 (2160p -> 1080p yuv422p10le bicubic) and config4 (stall frames).
 """
 import argparse
 import json
@@ -27,12 +40,28 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "processing-chain_amd"))
 
 FRAMES = 600
-SRC_W, SRC_H, DST_W, DST_H = 1280, 720, 1920, 1080
-SCALE_BYTES_PER_FRAME = 3_686_400 + 8_294_400     # 720p + 1080p yuv422p10le
-SITI_BYTES_PER_FRAME = 4_147_200                   # 1080p 10-bit luma, read once
 HBM_PEAK_GBS = 8000.0                              # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "1080p yuv422p10 AVPVS frames/sec + SI/TI frames/sec; achieved HBM GB/s"
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+# workload -> (src fmt, sw, sh, dst fmt, dw, dh, flags, siti luma (w, h) or None)
+WORKLOADS = {
+    "config2": ("yuv422p10le", 1280, 720, "yuv422p10le", 1920, 1080, "lanczos", (1920, 1080)),
+    "config3-10": ("yuv422p10le", 3840, 2160, "yuv422p10le", 1920, 1080, "bicubic", None),
+    "config3-8": ("yuv420p", 3840, 2160, "yuv422p10le", 1920, 1080, "bicubic", None),
+}
+DESCR = {
+    "config2": "config2 PVS: 10 s 1080p60 SRC -> SI/TI (1920x1080 10-bit luma) + 1280x720->1920x1080 "
+               "yuv422p10le lanczos AVPVS upscale",
+    "config3-10": "config3: 2160p60 yuv422p10le SRC -> 1920x1080 yuv422p10le (scale=1920:-2:flags=bicubic)",
+    "config3-8": "config3: 2160p60 yuv420p SRC -> 1920x1080 yuv422p10le (scale=1920:-2:flags=bicubic)",
+    "config4": "config4: stall frames (frozen 1080p yuv422p10le frame + spinner-128-white alpha blend)",
+}
+
+
+def frame_bytes(fmt, w, h):
+    from pixpath import formats
+    return formats.frame_bytes(fmt, w, h)
 
 
 def parse():
@@ -40,175 +69,334 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=FRAMES)
+    ap.add_argument("--frames", type=int, default=FRAMES, help="frames per PVS")
+    ap.add_argument("--pvs-per-rank", type=int, default=32)
+    ap.add_argument("--pvs-total", type=int, default=None, help="fixed batch size (strong scaling), e.g. 256")
+    ap.add_argument("--pool", type=int, default=8, help="distinct resident PVS inputs per rank")
+    ap.add_argument("--workload", default="config2", choices=sorted(list(WORKLOADS) + ["config4"]))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-frames", type=int, default=4096,
-                    help="upper bound on CPU-baseline frames (the sample also stops after --cpu-seconds)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-pipeline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="per CPU-baseline stage")
     ap.add_argument("--cpu-threads", type=int, default=16)
     return ap.parse_args()
 
 
-def cpu_baseline(args):
-    """Oracle C restatement on host threads (ctypes releases the GIL)."""
+def host_cpu():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count()
+    return model, os.cpu_count(), aff
+
+
+def cpu_baseline(args, wl):
+    """Oracle C restatement on host threads (ctypes releases the GIL); the
+    scaler and SI/TI are timed separately, the combined rate is per frame that
+    gets both (1 / (1/scale + 1/siti))."""
     import threading
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as po
+    sfmt, sw, sh, dfmt, dw, dh, flags, siti_wh = wl
+    model, nproc, aff = host_cpu()
+    nt = max(1, min(args.cpu_threads, aff))
     rng = np.random.default_rng(910)
-    n = args.cpu_sample_frames
-    nt = max(1, min(args.cpu_threads, n))
-    src = [[rng.integers(64, 941, (SRC_H, SRC_W)).astype(np.uint16),
-            rng.integers(64, 961, (SRC_H, SRC_W // 2)).astype(np.uint16),
-            rng.integers(64, 961, (SRC_H, SRC_W // 2)).astype(np.uint16)] for _ in range(nt)]
-    luma = [rng.integers(64, 941, (2, DST_H, DST_W)).astype(np.uint16) for _ in range(nt)]
-    sws = [po.Sws(po.YUV422P10LE, SRC_W, SRC_H, po.YUV422P10LE, DST_W, DST_H, po.SWS_LANCZOS) for _ in range(nt)]
+    sf, df = po.FMT_BY_NAME[sfmt], po.FMT_BY_NAME[dfmt]
+    depth = po.fmt_info(sf)[0]
+    hi = 1024 if depth > 8 else 256
+    src = [[rng.integers(0, hi, s).astype(po.plane_dtype(sf)) for s in po.plane_shapes(sf, sw, sh)]
+           for _ in range(nt)]
+    fl = {"lanczos": po.SWS_LANCZOS, "bicubic": po.SWS_BICUBIC}[flags]
+    sws = [po.Sws(sf, sw, sh, df, dw, dh, fl) for _ in range(nt)]
 
-    done = [0] * nt
+    def timed(fn):
+        done = [0] * nt
 
-    def work(t):
-        for i in range(t, n, nt):
-            sws[t].scale(src[t])
-            po.siti_c(luma[t], 10)  # 2 frames: SI of both, TI of the second
-            done[t] += 1
-            if time.perf_counter() - t0 > args.cpu_seconds:
-                break
+        def work(t):
+            while time.perf_counter() - t0 < args.cpu_seconds:
+                done[t] += fn(t)
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=work, args=(t,)) for t in range(nt)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        return sum(done), time.perf_counter() - t0
+
+    def do_scale(t):
+        sws[t].scale(src[t])
+        return 1
+    ns, ts = timed(do_scale)
+    scale_fps = ns / ts
+    out = {"unit": "frames/s", "cores": nt, "kind": "port", "host_nproc": nproc, "host_affinity": aff,
+           "cpu_model": model, "scale_fps": round(scale_fps, 2)}
+    if siti_wh:
+        w, h = siti_wh
+        luma = [rng.integers(0, 1024, (8, h, w)).astype(np.uint16) for _ in range(nt)]
+
+        def do_siti(t):
+            po.siti_c(luma[t], 10)  # 8 frames: 8 SI + 7 TI
+            return 8
+        nq, tq = timed(do_siti)
+        siti_fps = nq / tq
+        out["siti_fps"] = round(siti_fps, 2)
+        out["value"] = round(1.0 / (1.0 / scale_fps + 1.0 / siti_fps), 2)
+        out["sample"] = ("%d-thread oracle C restatement (oracle/pixoracle.c + siti_oracle.c, gcc -O3): %d frames "
+                         "%dx%d %s -> %dx%d %s %s in %.1f s, then %d frames of %dx%d 10-bit SI/TI in %.1f s; "
+                         "value = per frame that gets both; ffmpeg is absent on the box"
+                         % (nt, ns, sw, sh, sfmt, dw, dh, dfmt, flags, ts, nq, w, h, tq))
+    else:
+        out["value"] = round(scale_fps, 2)
+        out["sample"] = ("%d-thread oracle C restatement (gcc -O3): %d frames %dx%d %s -> %dx%d %s %s in %.1f s; "
+                         "ffmpeg is absent on the box" % (nt, ns, sw, sh, sfmt, dw, dh, dfmt, flags, ts))
+    return out
+
+
+def pcie_pipeline(wl, n_frames, dev):
+    """Pinned host frames -> H2D -> scaler -> D2H through pixpath.pipeline
+    (two streams, double buffers); PCIe-inclusive, reported beside `value`."""
+    import numpy as np
+    from pixpath import ops
+    from pixpath.pipeline import Pipeline, Stage
+    sfmt, sw, sh, dfmt, dw, dh, flags, _ = wl
+    in_fb, out_fb = frame_bytes(sfmt, sw, sh), frame_bytes(dfmt, dw, dh)
+    pool = np.random.default_rng(7).integers(0, 256, (8, in_fb), dtype=np.uint8)
+
+    class MemReader:
+        def __init__(self):
+            self.left = n_frames
+
+        def read_into(self, buf, n):
+            k = min(n, self.left)
+            b = np.frombuffer(buf, np.uint8).reshape(-1, in_fb)
+            for i in range(k):
+                b[i] = pool[(n_frames - self.left + i) % len(pool)]
+            self.left -= k
+            return k
+
+    class NullWriter:
+        def write(self, frames):
+            pass
+    sc = ops.Scaler(sfmt, sw, sh, dfmt, dw, dh, flags=flags, device=dev.index)
+    stage = Stage(sfmt, sw, sh, dfmt, dw, dh, lambda s, d, st: sc(s, d, stream=st))
+    pl = Pipeline(stage, batch=60, device=dev.index)
+    pl.run(MemReader(), NullWriter())  # warm-up pass (pinned buffers, plan)
+    import torch
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    th = [threading.Thread(target=work, args=(t,)) for t in range(nt)]
-    for x in th:
-        x.start()
-    for x in th:
-        x.join()
+    n = pl.run(MemReader(), NullWriter())
     dt = time.perf_counter() - t0
-    n = sum(done)
-    # each sample frame did one upscale and SI/TI of one frame (plus one extra SI)
-    return {"value": n / dt, "unit": "frames/s", "cores": nt, "kind": "port",
-            "sample": "%d frames, time-bounded at ~%gs (720p->1080p yuv422p10le lanczos + 1080p 10-bit SI/TI) on %d host threads, "
-                      "oracle/pixoracle.c + siti_oracle.c (gcc -O2); ffmpeg is absent on the box" % (n, args.cpu_seconds, nt),
-            "seconds": dt}
+    return {"frames_per_s": round(n / dt, 1), "pcie_gbs": round(n * (in_fb + out_fb) / dt / 1e9, 2),
+            "frames": n, "batch": 60,
+            "note": "host pinned -> H2D (copy stream) -> strip_kernel (compute stream) -> D2H -> host; "
+                    "host fill of the pinned input is included, decode/encode are not"}
+
+
+def make_inputs(wl, n, seed, dev):
+    import torch
+    from pixpath.frames import FrameBatch
+    sfmt, sw, sh, _, _, _, _, siti_wh = wl
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    src = FrameBatch(sfmt, sw, sh, n, device=dev)
+    depth = src.fmt.depth
+    rng_y = (64, 941) if depth > 8 else (16, 236)
+    rng_c = (64, 961) if depth > 8 else (16, 241)
+    for p, (lo, hi) in enumerate([rng_y, rng_c, rng_c]):
+        v = src.view(p)
+        v.copy_(torch.randint(lo, hi, v.shape, generator=g, device=dev, dtype=torch.int32).to(v.dtype))
+    luma = None
+    if siti_wh:
+        w, h = siti_wh
+        luma = torch.randint(64, 941, (n, h, w), generator=g, device=dev, dtype=torch.int32).to(torch.uint16)
+    return src, luma
 
 
 def main():
     args = parse()
+    from pixpath import batch
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # parent: start one rank per GPU and relay their exit status (no HIP here)
+        sys.exit(batch.spawn_local(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
+    rank, world, local = batch.rank_env()
+    if "WORLD_SIZE" in os.environ and args.gpus not in (1, world) and rank == 0:
+        print("bench: --gpus %d but WORLD_SIZE=%d; using the launcher's world" % (args.gpus, world), file=sys.stderr)
     import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+    batch.init_group(world)
+    dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.workload == "config4":
+        return bench_stall(args, rank, world, dev)
 
     from pixpath import ops
     from pixpath.frames import FrameBatch
-
+    wl = WORKLOADS[args.workload]
+    sfmt, sw, sh, dfmt, dw, dh, flags, siti_wh = wl
     n = args.frames
-    g = torch.Generator(device=dev)
-    g.manual_seed(910 + rank)
-    # synthetic inputs in the legal 10-bit range, generated in HBM
-    src = FrameBatch("yuv422p10le", SRC_W, SRC_H, n, device=dev)
-    for p, (lo, hi) in enumerate([(64, 941), (64, 961), (64, 961)]):
-        v = src.view(p)
-        v.copy_(torch.randint(lo, hi, v.shape, generator=g, device=dev, dtype=torch.int32).to(torch.uint16))
-    dst = FrameBatch("yuv422p10le", DST_W, DST_H, n, device=dev)
-    luma = torch.randint(64, 941, (n, DST_H, DST_W), generator=g, device=dev, dtype=torch.int32).to(torch.uint16)
-    scaler = ops.Scaler("yuv422p10le", SRC_W, SRC_H, "yuv422p10le", DST_W, DST_H, flags="lanczos")
+    total = args.pvs_total or world * args.pvs_per_rank
+    ids = ["PVS%03d" % i for i in range(total)]
+    mine = batch.my_pvs(ids, rank, world)
+    k_pool = max(1, min(args.pool, len(mine)))
+    pool = [make_inputs(wl, n, 910 + int(pid[3:]), dev) for pid in mine[:k_pool]]
+    outs = [FrameBatch(dfmt, dw, dh, n, device=dev) for _ in range(min(2, max(1, len(mine))))]
+    scaler = ops.Scaler(sfmt, sw, sh, dfmt, dw, dh, flags=flags)
     torch.cuda.synchronize()
 
     ev = []
 
     def step(timed):
-        if timed:
-            a, b, c = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-            a.record()
-            scaler(src, dst)
-            b.record()
-            ops.siti(luma, 10)
-            c.record()
-            ev.append((a, b, c))
+        res = []
+        for i, pid in enumerate(mine):
+            src, luma = pool[i % k_pool]
+            if timed:
+                a, b, c = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                a.record()
+            scaler(src, outs[i % len(outs)])
+            if timed:
+                b.record()
+            if luma is not None:
+                res.append(ops.siti(luma, 10))
+            if timed:
+                c.record()
+                ev.append((a, b, c))
+        gathered = None
+        if siti_wh:
+            si = torch.stack([r[0] for r in res]).cpu().numpy() if res else None
+            ti = torch.stack([r[1] for r in res]).cpu().numpy() if res else None
+            local_res = {pid: (si[i], ti[i]) for i, pid in enumerate(mine)}
+            gathered = batch.gather_results(local_res, rank, world)
         else:
-            scaler(src, dst)
-            ops.siti(luma, 10)
+            torch.cuda.synchronize()
+        return gathered
 
     for _ in range(args.warmup):
         step(False)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    batch.barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(True)
+        gathered = step(True)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    batch.barrier(world)
+    elapsed = batch.max_over_ranks(time.perf_counter() - t0, world)
 
-    scale_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / len(ev)
-    siti_ms = sum(b.elapsed_time(c) for _, b, c in ev) / len(ev)
-    ms_per_step = elapsed * 1000.0 / args.steps
-    value = world * n * args.steps / elapsed
+    scale_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(1, len(ev))
+    siti_ms = sum(b.elapsed_time(c) for _, b, c in ev) / max(1, len(ev)) if siti_wh else None
+    frames_total = total * n * args.steps
+    value = frames_total / elapsed
+    per_rank = batch.gather_values(len(mine), rank, world)
+    if rank != 0:
+        return 0
+    bytes_pf = frame_bytes(sfmt, sw, sh) + frame_bytes(dfmt, dw, dh)
+    achieved = bytes_pf * n / (scale_ms / 1000.0) / 1e9
+    traffic = None
+    if os.path.exists(PMC_FILE) and args.workload == "config2":
+        try:
+            pm = json.load(open(PMC_FILE))
+            k = pm.get("kernels", {}).get("strip_kernel")
+            if k and pm.get("frames_per_launch") == n:
+                traffic = k["hbm_bytes_per_launch"]
+        except (OSError, ValueError, KeyError):
+            traffic = None
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1000.0 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "strong" if args.pvs_total else "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic (seeded legal-range samples generated in HBM; %d distinct resident PVS inputs per rank)"
+                % k_pool,
+        "config": {
+            "workload": DESCR[args.workload],
+            "pvs_total": total, "pvs_per_rank": per_rank, "frames_per_pvs": n,
+            "frames_per_rank_per_step": [k * n for k in per_rank],
+            "parallelism": "pvs-sharded x%d (one process per GPU; gloo host gather of SI/TI, no RCCL)" % world,
+        },
+        "avpvs_fps_kernel": round(n / (scale_ms / 1000.0), 1),
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "strip_kernel (fused H+V polyphase over 256-column strips, one launch per 600-frame PVS)",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": bytes_pf * n,
+            "avg_launch_ms": round(scale_ms, 4),
+        },
+        "cpu_baseline": None,
+    }
+    if siti_wh:
+        luma_b = siti_wh[0] * siti_wh[1] * 2
+        out["siti_fps_kernel"] = round(n / (siti_ms / 1000.0), 1)
+        out["siti_kernel"] = {"avg_launch_ms": round(siti_ms, 4), "algorithmic_bytes_per_launch": luma_b * n,
+                              "achieved": round(luma_b * n / (siti_ms / 1000.0) / 1e9, 1),
+                              "frac": round(luma_b * n / (siti_ms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4)}
+        some = gathered[mine[0]] if gathered else None
+        if some is not None:
+            out["siti_gather"] = {"pvs": len(gathered), "example": {"pvs": mine[0], "SI": round(some["SI"], 4),
+                                                                   "TI": round(some["TI"], 4)}}
+    if world == 1 and not args.no_pipeline:
+        out["pcie_pipeline"] = pcie_pipeline(wl, 600, dev)
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, wl)
+    print(json.dumps(out), flush=True)
+    return 0
 
+
+def bench_stall(args, rank, world, dev):
+    """config 4: stall frames (frozen frame + spinner) composed on the GPU."""
+    import numpy as np
+    import torch
+    from pixpath import ops, spinner
+    from pixpath.frames import FrameBatch
+    w, h, n = 1920, 1080, args.frames
+    anim, delays = spinner.load_apng(os.path.join(ROOT, "tests", "golden", "spinner-128-white.png"))
+    ops.spinner_upload(anim, "yuv422p10le", device=dev.index)
+    src, _ = make_inputs(("yuv422p10le", w, h, None, 0, 0, None, None), 8, 404 + rank, dev)
+    dst = FrameBatch("yuv422p10le", w, h, n, device=dev)
+    src_idx = np.arange(n, dtype=np.int32) % 8
+    sp_idx = np.arange(n, dtype=np.int32) % len(anim)
+    ev = []
+    for i in range(args.warmup + args.steps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        ops.stall_compose(src, src_idx, sp_idx, dst=dst)
+        b.record()
+        if i >= args.warmup:
+            ev.append((a, b))
+    torch.cuda.synchronize()
+    ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    fb = frame_bytes("yuv422p10le", w, h)
+    achieved = 2 * fb * n / (ms / 1000.0) / 1e9
     if rank == 0:
-        achieved = SCALE_BYTES_PER_FRAME * n / (scale_ms / 1000.0) / 1e9
-        traffic = None
-        if os.path.exists(PMC_FILE):
-            try:
-                pm = json.load(open(PMC_FILE))
-                k = pm.get("kernels", {}).get("strip_kernel") or pm.get("kernels", {}).get("scale_kernel")
-                if k and pm.get("frames_per_launch") == n:
-                    traffic = k["hbm_bytes_per_launch"]
-            except Exception:
-                traffic = None
-        out = {
-            "metric": METRIC,
-            "value": round(value, 1),
-            "unit": "frames/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u16",
-            "data": "synthetic (seeded legal-range 10-bit noise, generated in HBM)",
-            "config": {
-                "workload": "config2: 10 s 1080p60 SRC -> SI/TI (1920x1080 10-bit luma) + 1280x720->1920x1080 "
-                            "yuv422p10le lanczos AVPVS upscale",
-                "frames_per_step_per_gpu": n,
-                "parallelism": "pvs-sharded x%d (one process per GPU, no data-path collective)" % world,
-            },
-            "avpvs_fps_kernel": round(world * n / (scale_ms / 1000.0), 1),
-            "siti_fps_kernel": round(world * n / (siti_ms / 1000.0), 1),
-            "siti_achieved_gbs": round(SITI_BYTES_PER_FRAME * n / (siti_ms / 1000.0) / 1e9, 1),
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "strip_kernel (fused H+V polyphase over 256-column strips, one launch per 600-frame batch)",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": SCALE_BYTES_PER_FRAME * n,
-                "avg_launch_ms": round(scale_ms, 4),
-            },
-            "cpu_baseline": None,
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline(args)
-            out["cpu_baseline"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in cb.items()}
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+        print(json.dumps({"metric": "stall frames/s (config 4)", "value": round(world * n / (ms / 1000.0), 1),
+                          "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+                          "vs_baseline": None, "dtype": "u16", "data": "synthetic",
+                          "config": {"workload": DESCR["config4"], "frames_per_launch": n},
+                          "roofline": {"bound": "hbm", "kernel": "stall_kernel", "achieved": round(achieved, 1),
+                                       "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                                       "traffic": None, "algorithmic_bytes_per_launch": 2 * fb * n,
+                                       "avg_launch_ms": round(ms, 4)},
+                          "cpu_baseline": None}), flush=True)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

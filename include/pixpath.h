@@ -107,6 +107,12 @@ int pp_scale_plan_filter(const pp_scale_plan *plan, int which, int16_t *coef,
  * environment variable PIXPATH_SCALE_KERNEL=generic at plan creation forces 0
  * (parity tests run both kernels on the same cases). */
 int pp_scale_plan_path(const pp_scale_plan *plan);
+/* Launch geometry of the plan for measurement and documentation: fills up to
+ * n of {LDS bytes per workgroup, threads per workgroup, workgroups per frame,
+ * luma chunk rows, luma segment rows, luma V tap pairs, chroma V tap pairs,
+ * luma staged columns, luma window rows, luma max new rows per chunk}.
+ * Returns the number of values written. */
+int pp_scale_plan_stats(const pp_scale_plan *plan, int64_t *out, int n);
 /* Run the plan on `nframes` device frames. */
 int pp_scale_execute(pp_scale_plan *plan, const pp_frames *src,
                      const pp_frames *dst, int nframes, void *stream);

@@ -28,132 +28,10 @@
 #include <memory>
 #include <type_traits>
 
-#include "common.hpp"
-#include "device.hpp"
 #include "filters.hpp"
+#include "scale_dev.hpp"
 
 namespace pp {
-
-constexpr int kTileW = 256;      // widest output tile (columns); narrower for large downscales
-constexpr int kThreads = 256;    // 4 waves
-constexpr int kLdsBudget = 40 * 1024;
-constexpr int kChoMax = 32;     // output rows per chunk (upper bound)
-constexpr int kSegRows = 256;   // output rows per segment (target)
-
-__constant__ uint8_t c_dither[8][8] = {
-    {36, 68, 60, 92, 34, 66, 58, 90},  {100, 4, 124, 28, 98, 2, 122, 26},
-    {52, 84, 44, 76, 50, 82, 42, 74},  {116, 20, 108, 12, 114, 18, 106, 10},
-    {32, 64, 56, 88, 38, 70, 62, 94},  {96, 0, 120, 24, 102, 6, 126, 30},
-    {48, 80, 40, 72, 54, 86, 46, 78},  {112, 16, 104, 8, 118, 22, 110, 14},
-};
-
-struct PlaneJob {
-    int sw, sh, dw, dh;
-    int tiles_x, tiles_y, tile_base;  // strips x vertical segments, first block index
-    int tw, twl, seg_h, cho; // strip width (= 1 << twl), output rows per segment, output rows per chunk
-    int vtp, ring, maxnew, S; // V tap pairs, window rows (even), staged rows per chunk, staged cols
-    int dither_off;       // 0 (Y, U) or 3 (V)
-    const int32_t *hpos;  // [dw]   window start (absolute source column)
-    const int16_t *hcoef; // [dw * HT]
-    const int32_t *vbase; // [dh]   first ring row of the window, rounded down to even
-    const int32_t *vcoef2; // [dh * vtp] tap pairs (rows base+2j, base+2j+1) packed lo|hi
-    const int32_t *tile_c0, *tile_cn; // [tiles_x] staged column window per strip
-    const int32_t *chunk_lo, *chunk_hi; // [ceil(dh/cho)] source rows needed by each chunk
-    // strip_kernel only
-    const int32_t *hbase4;  // [tiles_x * 64] 8-B aligned window base (staged-row sample) per 4-column lane
-    const int32_t *hcoefw;  // [tiles_x * 64][4][HW] taps re-laid over the lane's HW dwords (int16 pairs)
-    const int32_t *vrow16;  // [dh][16] per output row: window base row (even), then 8 tap pairs (zero padded)
-};
-
-struct ScaleArgs {
-    PlaneJob pl[3];
-    const uint8_t *src[3];
-    int64_t sls[3], sfs[3];
-    uint8_t *dst[3];
-    int64_t dls[3], dfs[3];
-    int nplanes;
-    int tiles;    // workgroups per frame (all planes)
-    int hshift;   // 7 for 8-bit sources, depth-1 otherwise
-    int dither;   // ordered dither (>8-bit source narrowed to 8 bit)
-    int vec_src;  // all source rows 16-B aligned
-    int vec_dst;  // all destination rows 8-B aligned (4 outputs per lane)
-};
-
-// Register prefetch of up to kPF 16-byte source chunks per lane (software
-// pipelining of the staging: issued before the vertical pass of the previous
-// chunk, committed to LDS after it).
-constexpr int kPF = 4;
-
-template <typename ST>
-struct Prefetch {
-    uint4 v[kPF];
-};
-
-// Unaligned-source fallback: element loads, zero past the plane edge.
-template <typename ST>
-__device__ inline uint4 load16_scalar(const ST *g, int col, int sw) {
-    constexpr int CH = 16 / sizeof(ST);
-    uint4 r = {0, 0, 0, 0};
-    ST tmp[CH];
-#pragma unroll
-    for (int e = 0; e < CH; ++e) tmp[e] = (col + e < sw) ? g[col + e] : ST(0);
-    __builtin_memcpy(&r, tmp, 16);
-    return r;
-}
-
-// Bounds-checked 16-B load through the frame plane's buffer resource: bytes at
-// or past num_records read as 0 without touching memory, so lanes with no
-// chunk (and the right edge of the plane's last row) need no branch.  Samples
-// past a row's end inside the plane come from the next row; the compacted
-// filters give them zero weight.
-__device__ inline uint4 bload16(__amdgpu_buffer_rsrc_t rs, int off) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-    uint4 r;
-    __builtin_memcpy(&r, &v, 16);
-    return r;
-}
-
-typedef int16_t v2i16 __attribute__((ext_vector_type(2)));
-
-// a.lo*b.lo + a.hi*b.hi + c in the VOP3P form (the compiler's v_dot2c form
-// needs the accumulator copied into the destination first)
-__device__ inline int dot2_acc(v2i16 a, v2i16 b, int c) {
-    int r;
-    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-
-// a.lo*b.lo + a.hi*b.hi with a zero accumulator as an inline constant (the
-// compiler otherwise zeroes a register for the v_dot2c form)
-__device__ inline int dot2_first(v2i16 a, v2i16 b) {
-    int r;
-    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-
-// 16-bit sources are stored as s ^ 0x8000 (= s - 32768 as int16) so any u16
-// sample is an exact signed operand of v_dot2_i32_i16; the H pass adds the
-// 32768 * sum(coef) bias back.  8-bit samples are stored as-is (<= 255).
-template <typename ST>
-__device__ inline void store16(uint16_t *lds_dst, uint4 v) {
-    if constexpr (sizeof(ST) == 2) {
-        v.x ^= 0x80008000u; v.y ^= 0x80008000u; v.z ^= 0x80008000u; v.w ^= 0x80008000u;
-        *reinterpret_cast<uint4 *>(lds_dst) = v;
-    } else {
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        uint4 lo, hi;
-        lo.x = __builtin_amdgcn_perm(0, w[0], 0x0c010c00u);
-        lo.y = __builtin_amdgcn_perm(0, w[0], 0x0c030c02u);
-        lo.z = __builtin_amdgcn_perm(0, w[1], 0x0c010c00u);
-        lo.w = __builtin_amdgcn_perm(0, w[1], 0x0c030c02u);
-        hi.x = __builtin_amdgcn_perm(0, w[2], 0x0c010c00u);
-        hi.y = __builtin_amdgcn_perm(0, w[2], 0x0c030c02u);
-        hi.z = __builtin_amdgcn_perm(0, w[3], 0x0c010c00u);
-        hi.w = __builtin_amdgcn_perm(0, w[3], 0x0c030c02u);
-        reinterpret_cast<uint4 *>(lds_dst)[0] = lo;
-        reinterpret_cast<uint4 *>(lds_dst)[1] = hi;
-    }
-}
 
 // TWC: 256 when every plane uses 256-column strips (the usual case: lane =
 // column, wave = row group, all row loops wave-uniform), 0 for the general
@@ -456,296 +334,6 @@ __global__ __launch_bounds__(kThreads) void scale_kernel(const ScaleArgs a) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// strip_kernel: the common-case scaler (every plane in 256-column strips,
-// 16-B aligned source rows, <= 8 vertical tap pairs, <= 10-bit samples).
-//
-// Same strip/segment/chunk walk and LDS layout as scale_kernel, but every
-// loop is wave-uniform (wave = row group, lane = 4 adjacent columns), so the
-// control flow is scalar branches instead of exec-mask bookkeeping:
-//   H pass: one lane computes 4 adjacent output columns of a row PAIR.  The 4
-//     windows share one 8-B aligned base in the staged row (hbase4), read as
-//     HW dwords with ds_read_b64 (one read serves all 4 outputs); per output
-//     the taps are re-laid over those dwords (hcoefw, zero outside its
-//     window), so each output is HW v_dot2_i32_i16 with no realignment, and
-//     the 8 results go to the window as one ds_write_b128.
-//   V pass: a wave owns an output row; its tap pairs come from a padded
-//     [dh][8] table through scalar loads (SGPR operands of v_dot2), the
-//     window rows through ds_read_b128 (4 columns x 2 rows), one 8-B store.
-//   Kept row pairs are read before the chunk's first barrier and written
-//     after it, so the move costs no extra barrier.
-// The next chunk's source rows are prefetched into registers right after the
-// first barrier, so their HBM latency overlaps both passes.
-#define kconst __attribute__((address_space(4)))  // constant address space: uniform loads become s_load
-template <typename T>
-__device__ inline const kconst T *as_kconst(const void *p) {
-    return (const kconst T *)(uintptr_t)p;
-}
-constexpr int kKeepRegs = 2;  // kept pairs per wave carried in registers (4 waves -> 8 pairs)
-
-template <typename ST>
-__device__ inline void store_raw16(uint16_t *lds_dst, uint4 v) {
-    if constexpr (sizeof(ST) == 2) {
-        *reinterpret_cast<uint4 *>(lds_dst) = v;  // <= 10-bit samples are exact int16 operands
-    } else {
-        store16<ST>(lds_dst, v);                  // 8-bit: widen to 16-bit
-    }
-}
-
-template <typename ST, int OUTB, int HW>
-__global__ __launch_bounds__(kThreads) void strip_kernel(const ScaleArgs a) {
-    extern __shared__ __align__(16) uint16_t lds[];
-    const int L = xcd_remap(blockIdx.x, gridDim.x);
-    const int frame = L / a.tiles;
-    int t = L - frame * a.tiles;
-    int p = 0;
-    if (a.nplanes > 1 && t >= a.pl[1].tile_base) p = 1;
-    if (a.nplanes > 2 && t >= a.pl[2].tile_base) p = 2;
-    const PlaneJob &J = a.pl[p];
-    t -= J.tile_base;
-    const int seg = t / J.tiles_x, tx = t - seg * J.tiles_x;
-    const int x0 = tx * kTileW, nx = min(kTileW, J.dw - x0);
-    const int c0 = as_kconst<int32_t>(J.tile_c0)[tx], cn = as_kconst<int32_t>(J.tile_cn)[tx];
-    // chunk tables through the scalar cache: no vector-memory wait at chunk starts
-    const kconst int32_t *chunk_lo = as_kconst<int32_t>(J.chunk_lo), *chunk_hi = as_kconst<int32_t>(J.chunk_hi);
-    const int S = J.S;
-    const int tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int lane = tid & 63;
-    const int cx = lane * 4;
-    uint16_t *src_t = lds;                                                  // [maxnew][S]
-    uint32_t *win = reinterpret_cast<uint32_t *>(lds + J.maxnew * S);       // [ring/2][256] row pairs
-    const ST *sbase = reinterpret_cast<const ST *>(a.src[p] + frame * a.sfs[p]);
-    uint8_t *dbase = a.dst[p] + frame * a.dfs[p];
-
-    // ---- horizontal taps of this lane's 4 columns over its HW-dword window ----
-    constexpr int hshift = sizeof(ST) == 1 ? 7 : 9;
-    const int g = tx * 64 + lane;
-    const int hb = J.hbase4[g];
-    v2i16 hc[4][HW];
-    {
-        const int4 *hp4 = reinterpret_cast<const int4 *>(J.hcoefw + (int64_t)g * 4 * HW);
-#pragma unroll
-        for (int i = 0; i < HW; ++i) {
-            const int4 v = hp4[i];
-            const int e[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) hc[(4 * i + q) / HW][(4 * i + q) % HW] = __builtin_bit_cast(v2i16, e[q]);
-        }
-        // consume the taps here, so their vmcnt wait is placed before the chunk
-        // loop (inside it, the wait would also cover the previous chunk's stores)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int d = 0; d < HW; ++d) asm volatile("" ::"v"(hc[j][d]));
-        asm volatile("" ::"v"(hb));
-    }
-
-    // ---- staging (16-B loads through the plane's buffer resource) ----------
-    constexpr int CH = 16 / sizeof(ST);
-    const int cpr = (cn + CH - 1) / CH;  // 16-B chunks per staged row (<= kThreads, host-checked)
-    const int64_t sls = a.sls[p];
-    const int sw = J.sw;
-    const int64_t last_row = std::min<int64_t>(sls, ((int64_t)sw * sizeof(ST) + 15) & ~int64_t(15));
-    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(sbase, (int)((int64_t)(J.sh - 1) * sls + last_row));
-    const int cbyte = c0 * (int)sizeof(ST);
-    const int s_rstep = kThreads / cpr;
-    const int s_r0 = tid / cpr, s_ch = tid - s_r0 * cpr;
-    const bool s_on = s_r0 < s_rstep;
-    const int s_lds = s_r0 * S + s_ch * CH;
-    const int s_goff = s_r0 * (int)sls + cbyte + s_ch * 16;
-    auto prefetch = [&](Prefetch<ST> &pf, int from, int hi_) {
-        const int nrow = hi_ - from;
-#pragma unroll
-        for (int k = 0; k < kPF; ++k) {
-            const int r = s_r0 + k * s_rstep;
-            pf.v[k] = bload16(rs, (s_on && r < nrow) ? s_goff + (from + k * s_rstep) * (int)sls : kOobOff);
-        }
-    };
-    auto commit = [&](const Prefetch<ST> &pf, int from, int hi_) {
-        const int nrow = hi_ - from;
-        if (!s_on) return;
-#pragma unroll
-        for (int k = 0; k < kPF; ++k)
-            if (s_r0 + k * s_rstep < nrow) store_raw16<ST>(src_t + s_lds + k * s_rstep * S, pf.v[k]);
-        for (int k = kPF; s_r0 + k * s_rstep < nrow; ++k)
-            store_raw16<ST>(src_t + s_lds + k * s_rstep * S, bload16(rs, s_goff + (from + k * s_rstep) * (int)sls));
-    };
-
-    // 4 outputs of one staged row (15-bit intermediates, hScale*To15 clip)
-    auto hrow4 = [&](const uint16_t *row, int out[4]) {
-        const uint16_t *sp = row + hb;
-        uint32_t w[HW];
-#pragma unroll
-        for (int d = 0; d + 1 < HW; d += 2) {
-            const uint2 v = *reinterpret_cast<const uint2 *>(sp + 2 * d);
-            w[d] = v.x;
-            w[d + 1] = v.y;
-        }
-        if constexpr (HW & 1) w[HW - 1] = *reinterpret_cast<const uint32_t *>(sp + 2 * (HW - 1));
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            int acc = dot2_first(__builtin_bit_cast(v2i16, w[0]), hc[j][0]);
-#pragma unroll
-            for (int d = 1; d < HW; ++d) acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, w[d]), hc[j][d], acc, false);
-            acc >>= hshift;
-            out[j] = acc < 32767 ? acc : 32767;
-        }
-    };
-
-    const int y_begin = seg * J.seg_h, y_end = min(J.dh, y_begin + J.seg_h);
-    const int cho = J.cho;
-    int next_src = chunk_lo[y_begin / cho];
-    int base = next_src & ~1;
-    Prefetch<ST> pf;
-    prefetch(pf, next_src, chunk_hi[y_begin / cho]);
-    const bool lane_any = cx < nx, lane_full = cx + 4 <= nx;
-    const int xo = x0 + cx;
-    const int64_t dls = a.dls[p];
-    const int vtp = J.vtp;
-    const kconst int32_t *vrow = as_kconst<int32_t>(J.vrow16);
-    for (int y0 = y_begin; y0 < y_end; y0 += cho) {
-        const int ci = y0 / cho;
-        const int lo = chunk_lo[ci], hi = chunk_hi[ci];
-        if (next_src < lo) next_src = lo;
-        const int nnew = hi - next_src;
-        const int nbase = lo & ~1;
-        const int keep = next_src > nbase ? (next_src - nbase + 1) >> 1 : 0;
-        const int shift = (nbase - base) >> 1;
-        // kept pairs: read now (other waves may still read them in the previous
-        // V pass), written down after the barrier
-        const bool keep_regs = keep <= 4 * kKeepRegs;
-        uint4 kp0 = {0, 0, 0, 0}, kp1 = {0, 0, 0, 0};  // pairs wave and wave + 4
-        if (shift > 0 && keep_regs) {
-            const int top = (J.ring >> 1) - 1;  // unconditional reads, clamped into the window
-            kp0 = *reinterpret_cast<const uint4 *>(win + min(wave + shift, top) * kTileW + cx);
-            kp1 = *reinterpret_cast<const uint4 *>(win + min(wave + 4 + shift, top) * kTileW + cx);
-        }
-        if (nnew > 0) commit(pf, next_src, hi);
-        __syncthreads();  // staged rows visible; every wave has left the previous V pass
-        const int after = nnew > 0 ? hi : next_src;
-        if (y0 + cho < y_end) prefetch(pf, max(after, chunk_lo[ci + 1]), chunk_hi[ci + 1]);
-        if (shift > 0) {
-            if (keep_regs) {
-                if (wave < keep) *reinterpret_cast<uint4 *>(win + wave * kTileW + cx) = kp0;
-                if (wave + 4 < keep) *reinterpret_cast<uint4 *>(win + (wave + 4) * kTileW + cx) = kp1;
-            } else {  // long windows (large downscales): column-sequential move
-                for (int k = 0; k < keep; ++k) win[k * kTileW + tid] = win[(k + shift) * kTileW + tid];
-                __syncthreads();
-            }
-        }
-        base = nbase;
-        // ---- horizontal pass: row pairs of the window, wave-strided ----------
-        if (nnew > 0) {
-            const int i0 = next_src - base;
-            const int kf0 = (i0 + 1) >> 1, kf1 = (i0 + nnew) >> 1;
-            if ((i0 & 1) && wave == ((i0 >> 1) & 3)) {  // high row of a kept pair (same wave moved it)
-                int o[4];
-                hrow4(src_t, o);
-                uint16_t *w16 = reinterpret_cast<uint16_t *>(win + (i0 >> 1) * kTileW + cx);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) w16[2 * j + 1] = static_cast<uint16_t>(o[j]);
-            }
-            if (((i0 + nnew) & 1) && wave == (kf1 & 3)) {  // low row of the last pair
-                int o[4];
-                hrow4(src_t + (nnew - 1) * S, o);
-                uint4 v;
-                v.x = o[0] & 0xffff; v.y = o[1] & 0xffff; v.z = o[2] & 0xffff; v.w = o[3] & 0xffff;
-                *reinterpret_cast<uint4 *>(win + kf1 * kTileW + cx) = v;
-            }
-            for (int k = kf0 + wave; k < kf1; k += 4) {
-                const int ra = 2 * k - i0;
-                int oa[4], ob[4];
-                hrow4(src_t + ra * S, oa);
-                hrow4(src_t + (ra + 1) * S, ob);
-                uint4 v;
-                v.x = __builtin_amdgcn_perm(ob[0], oa[0], 0x05040100u);
-                v.y = __builtin_amdgcn_perm(ob[1], oa[1], 0x05040100u);
-                v.z = __builtin_amdgcn_perm(ob[2], oa[2], 0x05040100u);
-                v.w = __builtin_amdgcn_perm(ob[3], oa[3], 0x05040100u);
-                *reinterpret_cast<uint4 *>(win + k * kTileW + cx) = v;
-            }
-            next_src = hi;
-        }
-        __syncthreads();  // window complete
-        // ---- vertical pass: one output row per wave --------------------------
-        const int ny = min(cho, y_end - y0);
-        // VT (= vtp) tap pairs, compile-time per instance: every window read of
-        // a row is in flight before the first v_dot2 waits on one
-        auto vpass = [&](auto vt_c) {
-            constexpr int VT = decltype(vt_c)::value;
-            const kconst int32_t *row = vrow + (int64_t)(y0 + wave) * 16;
-            uint8_t *drow_p = dbase + (int64_t)(y0 + wave) * dls;
-            for (int yy = wave; yy < ny; yy += 4, row += 64, drow_p += 4 * dls) {
-                const int y = y0 + yy;
-                // row tables through the scalar (constant) cache: SGPR operands
-                const int vb = (row[0] - nbase) >> 1;
-                const kconst int32_t *cp = row + 1;
-                const uint4 *rp = reinterpret_cast<const uint4 *>(win + vb * kTileW + cx);
-                uint4 q[VT];
-#pragma unroll
-                for (int j = 0; j < VT; ++j) q[j] = rp[j * (kTileW / 4)];
-                int acc[4];
-                if constexpr (OUTB == 8) {
-                    const int drow = y & 7;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        acc[j] = (a.dither ? c_dither[drow][(xo + j + J.dither_off) & 7] : 64) << 12;
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[j] = 1 << (10 + 16 - OUTB);
-                }
-#pragma unroll
-                for (int j = 0; j < VT; ++j) {
-                    const v2i16 c2 = __builtin_bit_cast(v2i16, cp[j]);
-                    acc[0] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].x), c2, acc[0], false);
-                    acc[1] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].y), c2, acc[1], false);
-                    acc[2] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].z), c2, acc[2], false);
-                    acc[3] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].w), c2, acc[3], false);
-                }
-                if (!lane_any) continue;
-                constexpr int sh = OUTB == 8 ? 19 : 11 + 16 - OUTB;
-                constexpr int mx = (1 << OUTB) - 1;
-                int o[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) o[j] = min(max(acc[j] >> sh, 0), mx);
-                if constexpr (OUTB == 8) {
-                    if (lane_full && a.vec_dst) {
-                        *reinterpret_cast<uint32_t *>(drow_p + xo) =
-                            (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | ((uint32_t)o[3] << 24);
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (xo + j < J.dw) drow_p[xo + j] = (uint8_t)o[j];
-                    }
-                } else {
-                    uint16_t *d16 = reinterpret_cast<uint16_t *>(drow_p);
-                    if (lane_full && a.vec_dst) {
-                        uint2 v;
-                        v.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-                        v.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-                        *reinterpret_cast<uint2 *>(d16 + xo) = v;
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (xo + j < J.dw) d16[xo + j] = (uint16_t)o[j];
-                    }
-                }
-            }
-        };
-        switch (vtp) {  // uniform, once per chunk
-        case 1: vpass(std::integral_constant<int, 1>{}); break;
-        case 2: vpass(std::integral_constant<int, 2>{}); break;
-        case 3: vpass(std::integral_constant<int, 3>{}); break;
-        case 4: vpass(std::integral_constant<int, 4>{}); break;
-        case 5: vpass(std::integral_constant<int, 5>{}); break;
-        case 6: vpass(std::integral_constant<int, 6>{}); break;
-        case 7: vpass(std::integral_constant<int, 7>{}); break;
-        default: vpass(std::integral_constant<int, 8>{}); break;
-        }
-    }
-}
-
 // planarCopyWrapper (same subsampling, same or wider depth): 8 samples per lane.
 __global__ __launch_bounds__(256) void copy_widen_kernel(const uint8_t *src, int64_t sls, int64_t sfs, int sbytes,
                                                          uint8_t *dst, int64_t dls, int64_t dfs, int dbytes,
@@ -791,7 +379,6 @@ __global__ __launch_bounds__(256) void interleave_uyvy_kernel(const uint8_t *Y, 
     }
 }
 
-using KernelFn = void (*)(const ScaleArgs);
 
 template <typename ST, int OUTB, int TWC>
 KernelFn pick_ht_tw(int ht) {
@@ -805,21 +392,6 @@ KernelFn pick_ht_tw(int ht) {
     case 16: return scale_kernel<ST, OUTB, 16, TWC>;
     case 24: return scale_kernel<ST, OUTB, 24, TWC>;
     case 32: return scale_kernel<ST, OUTB, 32, TWC>;
-    default: return nullptr;
-    }
-}
-
-template <typename ST, int OUTB>
-KernelFn pick_strip(int hw) {
-    switch (hw) {
-    case 3: return strip_kernel<ST, OUTB, 3>;
-    case 4: return strip_kernel<ST, OUTB, 4>;
-    case 5: return strip_kernel<ST, OUTB, 5>;
-    case 6: return strip_kernel<ST, OUTB, 6>;
-    case 8: return strip_kernel<ST, OUTB, 8>;
-    case 10: return strip_kernel<ST, OUTB, 10>;
-    case 12: return strip_kernel<ST, OUTB, 12>;
-    case 16: return strip_kernel<ST, OUTB, 16>;
     default: return nullptr;
     }
 }
@@ -1240,6 +812,19 @@ extern "C" int pp_scale_plan_path(const pp_scale_plan *P) {
     return (P->kind == pp_scale_plan::GENERIC || P->kind == pp_scale_plan::GENERIC_UYVY) ? P->fast_hw : 0;
 }
 
+extern "C" int pp_scale_plan_stats(const pp_scale_plan *P, int64_t *out, int n) {
+    if (!P || !out || n < 0) PP_FAIL(PP_ERR_INVALID, "null argument");
+    if (P->kind == pp_scale_plan::COPY || P->kind == pp_scale_plan::INTERLEAVE) return 0;
+    const bool strip = P->fast_hw > 0;
+    const pp::PlaneJob &L = strip ? P->fjob[0] : P->job[0];
+    const int64_t v[] = {(int64_t)(strip ? P->fast_lds : P->lds_bytes), strip ? pp::kStripThreads : pp::kThreads,
+                         P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y, L.cho, L.seg_h, L.vtp,
+                         P->job[1].vtp, L.S, L.ring, L.maxnew};
+    const int k = std::min<int>(n, (int)(sizeof(v) / sizeof(v[0])));
+    for (int i = 0; i < k; ++i) out[i] = v[i];
+    return k;
+}
+
 extern "C" int pp_scale_plan_filter(const pp_scale_plan *P, int which, int16_t *coef, int32_t *pos, int capacity) {
     if (!P || which < 0 || which > 3) PP_FAIL(PP_ERR_INVALID, "bad plan/which");
     if (P->kind == pp_scale_plan::COPY || P->kind == pp_scale_plan::INTERLEAVE) return 0;
@@ -1274,6 +859,7 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
     a.dither = allow_dither && P->si.depth > 8 && out_depth == 8;
     a.vec_src = 1;
     a.vec_dst = 1;
+    if (const char *e = std::getenv("PIXPATH_SCALE_DEBUG")) a.debug = atoi(e);
     for (int p = 0; p < 3; ++p) {
         a.vec_src &= aligned(a.src[p], a.sls[p], nframes > 1 ? a.sfs[p] : 0, 16);
         a.vec_dst &= aligned(a.dst[p], a.dls[p], nframes > 1 ? a.dfs[p] : 0, out_depth == 8 ? 4 : 8);
@@ -1284,10 +870,8 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
     if (P->fast_hw && a.vec_src) {
         for (int p = 0; p < 3; ++p) a.pl[p] = P->fjob[p];
         lds = P->fast_lds;
-        if (P->si.depth == 8)
-            k = out_depth == 8 ? pick_strip<uint8_t, 8>(P->fast_hw) : pick_strip<uint8_t, 10>(P->fast_hw);
-        else
-            k = out_depth == 8 ? pick_strip<uint16_t, 8>(P->fast_hw) : pick_strip<uint16_t, 10>(P->fast_hw);
+        const int vtm = strip_vtm_bucket(std::max(P->fjob[0].vtp, P->fjob[1].vtp));
+        k = P->si.depth == 8 ? pick_strip_u8(out_depth, P->fast_hw, vtm) : pick_strip_u16(out_depth, P->fast_hw, vtm);
     } else if (P->si.depth == 8) {
         k = out_depth == 8 ? pick_ht<uint8_t, 8>(P->ht, tw256) : pick_ht<uint8_t, 10>(P->ht, tw256);
     } else {

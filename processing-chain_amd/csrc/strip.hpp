@@ -1,0 +1,340 @@
+// strip_kernel: the common-case scaler (every plane in 256-column strips,
+// 16-B aligned source rows, <= 8 vertical tap pairs, <= 10-bit samples).
+// Included by strip_u16.hip / strip_u8.hip, which instantiate it per source
+// sample type; the launch code is in scale.hip.
+//
+// Same strip/segment/chunk walk and LDS layout as scale_kernel, but every
+// loop is wave-uniform (wave = row group, lane = 4 adjacent columns), so the
+// control flow is scalar branches instead of exec-mask bookkeeping:
+//   H pass: one lane computes 4 adjacent output columns of a row PAIR.  The 4
+//     windows share one 8-B aligned base in the staged row (hbase4), read as
+//     HW dwords with ds_read_b64 (one read serves all 4 outputs); per output
+//     the taps are re-laid over those dwords (hcoefw, zero outside its
+//     window), so each output is HW v_dot2_i32_i16 with no realignment, and
+//     the 8 results go to the window as one ds_write_b128.
+//   V pass: a wave owns an output row; the row records (window base row + tap
+//     pairs, a padded [dh][16] table) of several rows come through the scalar
+//     cache at once (SGPR operands of v_dot2, one exposed scalar-load latency
+//     per group of rows), the window rows through ds_read_b128 (4 columns x 2
+//     rows), one 8-B store per row.
+//   Staging: the next chunk's new source rows are loaded into registers right
+//     after the chunk-start barrier and written to LDS right after the window
+//     barrier (when the H pass has released the staging rows).  The wave
+//     issues no other vector-memory op in between, so the wait for those
+//     loads never covers its own V-pass stores (vmcnt counts loads and stores
+//     in issue order).
+// Measured (profiles/r2): the per-row dependent scalar load of the V-pass row
+// record and the register budget (104 VGPRs = 4 workgroups/CU) were what kept
+// the round-1 kernel at 0.50 of the HBM roofline.
+#pragma once
+#include "scale_dev.hpp"
+
+namespace pp {
+
+constexpr int kStripPF = 3;  // 16-B staging chunks per lane prefetched into registers
+struct StripPrefetch {
+    uint4 v[kStripPF];
+};
+
+// Waves per SIMD the register allocation is bounded for: 6 (80 VGPRs, the LDS
+// limit of the config-2 plan: 6 workgroups/CU) where that needs no spill,
+// else 4 (128 VGPRs) or 3 (168 VGPRs, the widest H windows).  tools/check_spills.sh checks every instance.
+template <int SB, int OUTB, int HW, int VTM>
+constexpr int strip_min_waves() {
+    return HW >= 12 ? 3 : (VTM <= 5 && HW <= (OUTB == 10 && SB == 2 ? 6 : 4)) ? 6 : 4;
+}
+
+template <typename ST, int OUTB, int HW, int VTM>
+__global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
+    extern __shared__ __align__(16) uint16_t lds[];
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int frame = L / a.tiles;
+    int t = L - frame * a.tiles;
+    int p = 0;
+    if (a.nplanes > 1 && t >= a.pl[1].tile_base) p = 1;
+    if (a.nplanes > 2 && t >= a.pl[2].tile_base) p = 2;
+    const PlaneJob &J = a.pl[p];
+    t -= J.tile_base;
+    const int seg = t / J.tiles_x, tx = t - seg * J.tiles_x;
+    const int x0 = tx * kTileW, nx = min(kTileW, J.dw - x0);
+    const int c0 = as_kconst<int32_t>(J.tile_c0)[tx], cn = as_kconst<int32_t>(J.tile_cn)[tx];
+    // chunk tables through the scalar cache: no vector-memory wait at chunk starts
+    const kconst int32_t *chunk_lo = as_kconst<int32_t>(J.chunk_lo), *chunk_hi = as_kconst<int32_t>(J.chunk_hi);
+    const int S = J.S;
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int cx = lane * 4;
+    uint16_t *src_t = lds;                                                  // [maxnew][S]
+    uint32_t *win = reinterpret_cast<uint32_t *>(lds + J.maxnew * S);       // [ring/2][256] row pairs
+    const ST *sbase = reinterpret_cast<const ST *>(a.src[p] + frame * a.sfs[p]);
+    uint8_t *dbase = a.dst[p] + frame * a.dfs[p];
+
+    // ---- horizontal taps of this lane's 4 columns over its HW-dword window ----
+    constexpr int hshift = sizeof(ST) == 1 ? 7 : 9;
+    const int g = tx * 64 + lane;
+    const int hb = J.hbase4[g];
+    v2i16 hc[4][HW];
+    {
+        const int4 *hp4 = reinterpret_cast<const int4 *>(J.hcoefw + (int64_t)g * 4 * HW);
+#pragma unroll
+        for (int i = 0; i < HW; ++i) {
+            const int4 v = hp4[i];
+            const int e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) hc[(4 * i + q) / HW][(4 * i + q) % HW] = __builtin_bit_cast(v2i16, e[q]);
+        }
+        // consume the taps here, so their vmcnt wait is placed before the chunk
+        // loop (inside it, the wait would also cover the previous chunk's stores)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int d = 0; d < HW; ++d) asm volatile("" ::"v"(hc[j][d]));
+        asm volatile("" ::"v"(hb));
+    }
+
+    // ---- staging (16-B loads through the plane's buffer resource) ----------
+    constexpr int CH = 16 / sizeof(ST);
+    const int cpr = (cn + CH - 1) / CH;  // 16-B chunks per staged row (<= kThreads, host-checked)
+    const int64_t sls = a.sls[p];
+    const int sw = J.sw;
+    const int64_t last_row = std::min<int64_t>(sls, ((int64_t)sw * sizeof(ST) + 15) & ~int64_t(15));
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(sbase, (int)((int64_t)(J.sh - 1) * sls + last_row));
+    const int cbyte = c0 * (int)sizeof(ST);
+    const int s_rstep = kThreads / cpr;
+    const int s_r0 = tid / cpr, s_ch = tid - s_r0 * cpr;
+    const bool s_on = s_r0 < s_rstep;
+    const int s_lds = s_r0 * S + s_ch * CH;
+    const int s_goff = s_r0 * (int)sls + cbyte + s_ch * 16;
+    auto prefetch = [&](StripPrefetch &pf, int from, int hi_) {
+        const int nrow = hi_ - from;
+#pragma unroll
+        for (int k = 0; k < kStripPF; ++k) {
+            const int r = s_r0 + k * s_rstep;
+            pf.v[k] = bload16(rs, (s_on && r < nrow) ? s_goff + (from + k * s_rstep) * (int)sls : kOobOff);
+        }
+    };
+    auto commit = [&](const StripPrefetch &pf, int from, int hi_) {
+        const int nrow = hi_ - from;
+        if (!s_on) return;
+#pragma unroll
+        for (int k = 0; k < kStripPF; ++k)
+            if (s_r0 + k * s_rstep < nrow) store_raw16<ST>(src_t + s_lds + k * s_rstep * S, pf.v[k]);
+        for (int k = kStripPF; s_r0 + k * s_rstep < nrow; ++k)
+            store_raw16<ST>(src_t + s_lds + k * s_rstep * S, bload16(rs, s_goff + (from + k * s_rstep) * (int)sls));
+    };
+
+    // 4 outputs of one staged row (15-bit intermediates, hScale*To15 clip)
+    auto hrow4 = [&](const uint16_t *row, int out[4]) {
+        const uint16_t *sp = row + hb;
+        uint32_t w[HW];
+#pragma unroll
+        for (int d = 0; d + 1 < HW; d += 2) {
+            const uint2 v = *reinterpret_cast<const uint2 *>(sp + 2 * d);
+            w[d] = v.x;
+            w[d + 1] = v.y;
+        }
+        if constexpr (HW & 1) w[HW - 1] = *reinterpret_cast<const uint32_t *>(sp + 2 * (HW - 1));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            int acc = dot2_first(__builtin_bit_cast(v2i16, w[0]), hc[j][0]);
+#pragma unroll
+            for (int d = 1; d < HW; ++d) acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, w[d]), hc[j][d], acc, false);
+            acc >>= hshift;
+            out[j] = acc < 32767 ? acc : 32767;
+        }
+    };
+
+    const int y_begin = seg * J.seg_h, y_end = min(J.dh, y_begin + J.seg_h);
+    const int cho = J.cho;
+    int next_src = chunk_lo[y_begin / cho];
+    int base = next_src & ~1;
+    StripPrefetch pf;
+    // the first chunk's rows are staged before the loop; every later chunk's
+    // rows are loaded right after the chunk-start barrier of the chunk before
+    // and written to LDS right after its window barrier (src_t is free then).
+    // Between those two points the wave issues no vector-memory op, so the
+    // wait for the loads never covers this wave's V-pass stores (vmcnt is
+    // in-order over loads and stores).
+    prefetch(pf, next_src, chunk_hi[y_begin / cho]);
+    commit(pf, next_src, chunk_hi[y_begin / cho]);
+    const bool lane_any = cx < nx, lane_full = cx + 4 <= nx;
+    const int xo = x0 + cx;
+    const int64_t dls = a.dls[p];
+    const int vtp = J.vtp;
+    const kconst int32_t *vrow = as_kconst<int32_t>(J.vrow16);
+    for (int y0 = y_begin; y0 < y_end; y0 += cho) {
+        const int ci = y0 / cho;
+        const int lo = chunk_lo[ci], hi = chunk_hi[ci];
+        if (next_src < lo) next_src = lo;
+        const int nnew = hi - next_src;
+        const int nbase = lo & ~1;
+        const int keep = next_src > nbase ? (next_src - nbase + 1) >> 1 : 0;
+        const int shift = (nbase - base) >> 1;
+        if (!(a.debug & 8)) __syncthreads();  // staged rows visible; every wave has left the previous V pass
+        const int after = nnew > 0 ? hi : next_src;
+        const bool more = y0 + cho < y_end;
+        const int nfrom = more ? max(after, chunk_lo[ci + 1]) : 0, nhi = more ? chunk_hi[ci + 1] : 0;
+        if (more && !(a.debug & 2)) prefetch(pf, nfrom, nhi);
+        // kept row pairs move down to the window start, each column by its own
+        // lane in increasing order (no lane reads a slot already overwritten)
+        if (shift > 0) {
+            for (int k = 0; k < keep; ++k) win[k * kTileW + tid] = win[(k + shift) * kTileW + tid];
+            __syncthreads();
+        }
+        base = nbase;
+        // ---- horizontal pass: row pairs of the window, wave-strided ----------
+        if (nnew > 0 && (a.debug & 4)) next_src = hi;
+        if (nnew > 0 && !(a.debug & 4)) {
+            const int i0 = next_src - base;
+            const int kf0 = (i0 + 1) >> 1, kf1 = (i0 + nnew) >> 1;
+            if ((i0 & 1) && wave == ((i0 >> 1) & 3)) {  // high row of a kept pair (same wave moved it)
+                int o[4];
+                hrow4(src_t, o);
+                uint16_t *w16 = reinterpret_cast<uint16_t *>(win + (i0 >> 1) * kTileW + cx);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) w16[2 * j + 1] = static_cast<uint16_t>(o[j]);
+            }
+            if (((i0 + nnew) & 1) && wave == (kf1 & 3)) {  // low row of the last pair
+                int o[4];
+                hrow4(src_t + (nnew - 1) * S, o);
+                uint4 v;
+                v.x = o[0] & 0xffff; v.y = o[1] & 0xffff; v.z = o[2] & 0xffff; v.w = o[3] & 0xffff;
+                *reinterpret_cast<uint4 *>(win + kf1 * kTileW + cx) = v;
+            }
+            for (int k = kf0 + wave; k < kf1; k += 4) {
+                const int ra = 2 * k - i0;
+                int oa[4], ob[4];
+                hrow4(src_t + ra * S, oa);
+                hrow4(src_t + (ra + 1) * S, ob);
+                uint4 v;
+                v.x = __builtin_amdgcn_perm(ob[0], oa[0], 0x05040100u);
+                v.y = __builtin_amdgcn_perm(ob[1], oa[1], 0x05040100u);
+                v.z = __builtin_amdgcn_perm(ob[2], oa[2], 0x05040100u);
+                v.w = __builtin_amdgcn_perm(ob[3], oa[3], 0x05040100u);
+                *reinterpret_cast<uint4 *>(win + k * kTileW + cx) = v;
+            }
+            next_src = hi;
+        }
+        if (!(a.debug & 8)) __syncthreads();  // window complete; src_t is free
+        if (more && nhi > nfrom && !(a.debug & 2)) commit(pf, nfrom, nhi);
+        // ---- vertical pass: one output row per wave --------------------------
+        const int ny = min(cho, y_end - y0);
+        // VT (= vtp) tap pairs, compile-time per instance: every window read of
+        // a row is in flight before the first v_dot2 waits on one
+        auto vpass = [&](auto vt_c) {
+            constexpr int VT = decltype(vt_c)::value;
+            // row records (window base row + VT tap pairs) of G rows at a time
+            // through the scalar cache: one exposed scalar-load latency per
+            // group, not per row (the ds_reads of a row depend on its base)
+            constexpr int G = VT <= 2 ? 8 : VT <= 5 ? 4 : 2;
+            for (int g0 = wave; g0 < ny; g0 += 4 * G) {
+                int vb[G];
+                int32_t cf[G][VT];
+#pragma unroll
+                for (int i = 0; i < G; ++i) {
+                    const int rr = min(g0 + 4 * i, ny - 1);  // clamped: loads stay inside the table
+                    const kconst int32_t *row = vrow + (int64_t)(y0 + rr) * 16;
+                    vb[i] = row[0];
+#pragma unroll
+                    for (int j = 0; j < VT; ++j) cf[i][j] = row[1 + j];
+                }
+#pragma unroll
+                for (int i = 0; i < G; ++i) {
+                    const int yy = g0 + 4 * i;
+                    if (yy >= ny) break;
+                    const int y = y0 + yy;
+                    uint8_t *drow_p = dbase + (int64_t)y * dls;
+                    const uint4 *rp = reinterpret_cast<const uint4 *>(win + ((vb[i] - nbase) >> 1) * kTileW + cx);
+                    uint4 q[VT];
+#pragma unroll
+                    for (int j = 0; j < VT; ++j) q[j] = rp[j * (kTileW / 4)];
+                    int acc[4];
+                    if constexpr (OUTB == 8) {
+                        const int drow = y & 7;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            acc[j] = (a.dither ? c_dither[drow][(xo + j + J.dither_off) & 7] : 64) << 12;
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc[j] = 1 << (10 + 16 - OUTB);
+                    }
+#pragma unroll
+                    for (int j = 0; j < VT; ++j) {
+                        const v2i16 c2 = __builtin_bit_cast(v2i16, cf[i][j]);
+                        acc[0] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].x), c2, acc[0], false);
+                        acc[1] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].y), c2, acc[1], false);
+                        acc[2] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].z), c2, acc[2], false);
+                        acc[3] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].w), c2, acc[3], false);
+                    }
+                    if (!lane_any || (a.debug & 1)) continue;
+                    constexpr int sh = OUTB == 8 ? 19 : 11 + 16 - OUTB;
+                    constexpr int mx = (1 << OUTB) - 1;
+                    int o[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) o[j] = min(max(acc[j] >> sh, 0), mx);
+                    if constexpr (OUTB == 8) {
+                        if (lane_full && a.vec_dst) {
+                            *reinterpret_cast<uint32_t *>(drow_p + xo) =
+                                (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | ((uint32_t)o[3] << 24);
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                if (xo + j < J.dw) drow_p[xo + j] = (uint8_t)o[j];
+                        }
+                    } else {
+                        uint16_t *d16 = reinterpret_cast<uint16_t *>(drow_p);
+                        if (lane_full && a.vec_dst) {
+                            uint2 v;
+                            v.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+                            v.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+                            *reinterpret_cast<uint2 *>(d16 + xo) = v;
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                if (xo + j < J.dw) d16[xo + j] = (uint16_t)o[j];
+                        }
+                    }
+                    // keep the next row's window reads behind this row's math
+                    // (hoisting them all costs ~50 VGPRs and two waves/SIMD)
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        };
+        switch (vtp) {  // uniform, once per chunk; arms up to VTM only (register budget)
+        case 1: vpass(std::integral_constant<int, 1>{}); break;
+        case 2: if constexpr (VTM >= 2) vpass(std::integral_constant<int, 2>{}); break;
+        case 3: if constexpr (VTM >= 3) vpass(std::integral_constant<int, 3>{}); break;
+        case 4: if constexpr (VTM >= 4) vpass(std::integral_constant<int, 4>{}); break;
+        case 5: if constexpr (VTM >= 5) vpass(std::integral_constant<int, 5>{}); break;
+        case 6: if constexpr (VTM >= 6) vpass(std::integral_constant<int, 6>{}); break;
+        case 7: if constexpr (VTM >= 7) vpass(std::integral_constant<int, 7>{}); break;
+        default: if constexpr (VTM >= 8) vpass(std::integral_constant<int, 8>{}); break;
+        }
+    }
+}
+
+
+inline int strip_vtm_bucket_impl(int vtp) { return vtp <= 2 ? 2 : vtp <= 3 ? 3 : vtp <= 5 ? 5 : 8; }
+
+#define PP_STRIP_VTM(ST, OUTB, HW)                                           \
+    switch (vtm) {                                                           \
+    case 2: return strip_kernel<ST, OUTB, HW, 2>;                            \
+    case 3: return strip_kernel<ST, OUTB, HW, 3>;                            \
+    case 5: return strip_kernel<ST, OUTB, HW, 5>;                            \
+    default: return strip_kernel<ST, OUTB, HW, 8>;                           \
+    }
+#define PP_STRIP_HW(ST, OUTB)                                                \
+    switch (hw) {                                                            \
+    case 3: PP_STRIP_VTM(ST, OUTB, 3)                                        \
+    case 4: PP_STRIP_VTM(ST, OUTB, 4)                                        \
+    case 5: PP_STRIP_VTM(ST, OUTB, 5)                                        \
+    case 6: PP_STRIP_VTM(ST, OUTB, 6)                                        \
+    case 8: PP_STRIP_VTM(ST, OUTB, 8)                                        \
+    case 10: PP_STRIP_VTM(ST, OUTB, 10)                                      \
+    case 12: PP_STRIP_VTM(ST, OUTB, 12)                                      \
+    case 16: PP_STRIP_VTM(ST, OUTB, 16)                                      \
+    default: return nullptr;                                                 \
+    }
+
+}  // namespace pp

@@ -1,0 +1,13 @@
+// strip_kernel instances for 8-bit source samples (see strip.hpp).
+#include "strip.hpp"
+
+namespace pp {
+
+KernelFn pick_strip_u8(int outb, int hw, int vtm) {
+    if (outb == 8) {
+        PP_STRIP_HW(uint8_t, 8)
+    }
+    PP_STRIP_HW(uint8_t, 10)
+}
+
+}  // namespace pp

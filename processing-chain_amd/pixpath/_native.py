@@ -16,7 +16,7 @@ ERRORS = {-1: "PP_ERR_INVALID", -2: "PP_ERR_HIP", -3: "PP_ERR_NOMEM", -4: "PP_ER
 EXPORTS = (
     "pp_abi_version", "pp_last_error", "pp_ctx_create", "pp_ctx_destroy", "pp_plane_bytes",
     "pp_v210_linesize", "pp_scale_plan_create", "pp_scale_plan_destroy", "pp_scale_plan_filter",
-    "pp_scale_plan_path", "pp_scale_execute", "pp_pad_execute", "pp_v210_pack", "pp_cpvs_execute", "pp_spinner_upload", "pp_stall_compose",
+    "pp_scale_plan_path", "pp_scale_plan_stats", "pp_scale_execute", "pp_pad_execute", "pp_v210_pack", "pp_cpvs_execute", "pp_spinner_upload", "pp_stall_compose",
     "pp_siti", "pp_fps_map",
 )
 
@@ -61,6 +61,7 @@ def lib():
         "pp_scale_plan_destroy": (i32, [vp]),
         "pp_scale_plan_filter": (i32, [vp, i32, vp, vp, i32]),
         "pp_scale_plan_path": (i32, [vp]),
+        "pp_scale_plan_stats": (i32, [vp, vp, i32]),
         "pp_scale_execute": (i32, [vp, fr, fr, i32, vp]),
         "pp_pad_execute": (i32, [vp, i32, i32, i32, fr, i32, i32, i32, i32, fr, i32, vp]),
         "pp_v210_pack": (i32, [vp, i32, i32, fr, fr, i32, vp]),

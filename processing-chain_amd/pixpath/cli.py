@@ -11,9 +11,9 @@ the ffmpeg strings they replace).
   siti   P.910 SI/TI of a SRC (util/SRC_analysis.py hook)
 
 Inputs/outputs ending in .y4m or .raw/.yuv are read/written directly;
-anything else goes through ffmpeg pipes.  The device is chosen by
-PIXPATH_DEVICE, else by process id modulo the visible GPU count (one process
-per GPU under the reference's ParallelRunner).
+anything else goes through ffmpeg pipes.  The device is PIXPATH_DEVICE, else
+LOCAL_RANK, else the lowest free GPU slot (pixpath.devslot: the first N
+processes of the reference's ParallelRunner pool get N different GPUs).
 """
 import argparse
 import ast
@@ -27,11 +27,12 @@ import numpy as np
 
 def _device():
     import torch
+
+    from .devslot import choose_device
     n = torch.cuda.device_count()
     if n == 0:
         raise SystemExit("pixpath: no GPU visible")
-    d = os.environ.get("PIXPATH_DEVICE")
-    return int(d) if d is not None else os.getpid() % n
+    return choose_device(n)
 
 
 class CountingWriter:

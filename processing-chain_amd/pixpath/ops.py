@@ -41,7 +41,9 @@ class Context:
 def context(device=None):
     if device is None:
         device = torch.cuda.current_device()
-    device = torch.device("cuda", device).index if not isinstance(device, int) else device
+    if isinstance(device, torch.device):
+        device = device.index if device.index is not None else torch.cuda.current_device()
+    device = int(device)
     if device not in _contexts:
         _contexts[device] = Context(device)
     return _contexts[device]
@@ -85,6 +87,15 @@ class Scaler:
     def kernel_path(self):
         """> 0: the strip kernel runs (its H window in dwords); 0: the general kernel."""
         return check(lib().pp_scale_plan_path(self.handle))
+
+    @property
+    def stats(self):
+        """Launch geometry (pp_scale_plan_stats) as a dict."""
+        keys = ("lds_bytes", "threads", "tiles_per_frame", "cho", "seg_rows", "vtp_luma", "vtp_chroma",
+                "staged_cols", "window_rows", "max_new_rows")
+        v = np.zeros(len(keys), dtype=np.int64)
+        n = check(lib().pp_scale_plan_stats(self.handle, v.ctypes.data, len(keys)))
+        return dict(zip(keys[:n], (int(x) for x in v[:n])))
 
     def filter(self, which):
         """FFmpeg-layout filter (coef [n, size] int16, pos [n] int32) or None (unscaled path)."""

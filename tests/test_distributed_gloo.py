@@ -73,3 +73,57 @@ def test_assign_pvs_balanced_and_complete():
     parts = shard.assign_pvs(items, 8, cost=cost.get)
     loads = [sum(cost[i] for i in p) for p in parts]
     assert max(loads) - min(loads) <= 5
+
+
+# ---- the launcher bench.py uses (pixpath.batch), driven for real on CPU -----
+def test_spawn_local_two_ranks_gather_equals_single_pass(tmp_path):
+    """`bench.py --gpus 2` path: the parent spawns 2 ranks (RANK/LOCAL_RANK/
+    WORLD_SIZE/MASTER_*), each takes its PVS share, SI/TI is gathered over gloo
+    to rank 0 and equals the single-process result for every PVS."""
+    import sys
+    from pixpath import batch
+    out = tmp_path / "res.npz"
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join(sys.path))
+    rc = batch.spawn_local(2, [sys.executable, "-m", "pixpath.batch", "--selftest", str(out), "6"], env=env)
+    assert rc == 0
+    r = np.load(out)
+    assert int(r["world"]) == 2
+    assert list(r["ids"]) == ["PVS%03d" % i for i in range(6)]
+    assert sorted(set(r["ranks"].tolist())) == [0, 1]
+    assert np.bincount(r["ranks"]).tolist() == [3, 3]
+    for i in range(6):
+        si, ti = siti_ref.siti(batch._selftest_frames(i))
+        np.testing.assert_array_equal(r["si"][i], si)
+        np.testing.assert_array_equal(r["ti"][i][1:], ti[1:])
+        assert r["SI"][i] == si.max() and r["TI"][i] == np.nanmax(ti)
+
+
+def test_spawn_local_reports_failure(tmp_path):
+    import sys
+    from pixpath import batch
+    rc = batch.spawn_local(2, [sys.executable, "-c", "import os,sys; sys.exit(3 if os.environ['RANK']=='1' else 0)"])
+    assert rc == 3
+
+
+def test_my_pvs_config5_split():
+    from pixpath import batch
+    ids = ["PVS%03d" % i for i in range(256)]
+    parts = [batch.my_pvs(ids, r, 8) for r in range(8)]
+    assert sorted(sum(parts, [])) == ids and {len(p) for p in parts} == {32}
+
+
+def test_device_slots_spread_over_gpus(tmp_path):
+    """pixpath.cli processes under a Pool(-p 4) on 2 GPUs: devices 0,1,0,1 (not pid % n)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, PIXPATH_SLOT_DIR=str(tmp_path), PYTHONPATH=os.pathsep.join(sys.path))
+    procs = []
+    for _ in range(4):
+        procs.append(subprocess.Popen([sys.executable, "-m", "pixpath.devslot", "2", "3"], env=env,
+                                      stdout=subprocess.PIPE, text=True))
+        # wait until this process holds its slot before starting the next
+        procs[-1].stdout_line = procs[-1].stdout.readline().strip()
+    devs = sorted(int(p.stdout_line) for p in procs)
+    for p in procs:
+        p.wait()
+    assert devs == [0, 0, 1, 1]
