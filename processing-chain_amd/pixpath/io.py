@@ -212,8 +212,10 @@ def open_reader(path, f=None, w=None, h=None, rate=None):
 
 
 def probe(path):
-    """ffprobe stream info + packet-size sums (the reference's get_src_info /
-    get_stream_size, lib/ffmpeg.py:566-633, :399-417); Y4M files are parsed."""
+    """Decode-side stream description for the readers: Y4M headers are parsed,
+    anything else is asked of ffprobe (raw r_frame_rate, e.g. "60000/1001").
+    The reference's metadata calls (get_src_info / get_stream_size /
+    get_segment_info, with their normalisations) are pixpath.probe."""
     if path.lower().endswith(".y4m"):
         r = Y4MReader(path)
         st = {"width": r.w, "height": r.h, "coded_width": r.w, "coded_height": r.h, "pix_fmt": r.fmt.name,
@@ -230,12 +232,3 @@ def probe(path):
                             "-of", "compact=p=0:nk=1", path], check=True, capture_output=True).stdout.decode()
         sizes[sw] = sum(int(x) for x in o.split("\n") if x)
     return {"stream": st, "sizes": sizes}  # pragma: no cover
-
-
-def segment_info(path):
-    """The subset of get_segment_info (lib/ffmpeg.py:433-563) that get_difficulty reads."""
-    st = probe(path)["stream"]
-    dur = float(st.get("duration", 0.0))
-    return {"file_size": os.path.getsize(path), "video_duration": dur,
-            "video_frame_rate": float(Fraction(st["r_frame_rate"])), "video_width": st["width"],
-            "video_height": st["height"]}

@@ -49,6 +49,7 @@ class Pipeline:
         ``emit(k_global, n)`` -> list of (batch-local index) to write for input frame k
         (fps maps duplicate / drop frames on the host); default: each frame once."""
         B = self.batch
+        self.frames_in = self.frames_out = 0  # counts of this run
         rq = queue.Queue(maxsize=2)   # (slot, n) filled buffers
         free_in = queue.Queue()
         for i in range(2):
@@ -86,8 +87,12 @@ class Pipeline:
                                 writer.write(buf[i:i + 1])
                     self.frames_out += n
                     out_free[slot].set()
-            except Exception as e:
+            except Exception as e:  # e.g. the encoder died: release the producer and drain
                 err.append(e)
+                for ev in out_free:
+                    ev.set()
+                while wq.get() is not None:
+                    pass
 
         out_free = [threading.Event(), threading.Event()]
         for e in out_free:
@@ -99,11 +104,14 @@ class Pipeline:
         base = 0
         while True:
             slot, n = rq.get()
-            if slot is None or n == 0:
+            if slot is None or n == 0 or err:
                 if slot is not None:
                     free_in.put(slot)
                 break
             out_free[slot].wait()
+            if err:  # the writer failed while this slot was in use
+                free_in.put(slot)
+                break
             out_free[slot].clear()
             with torch.cuda.stream(self.copy_stream):
                 self.d_in[slot].storage[:n].copy_(self.h_in[slot][:n], non_blocking=True)

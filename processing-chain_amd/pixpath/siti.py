@@ -2,9 +2,10 @@
 
 Mirrors util/SRC_analysis.py (md5sum :33-43, sum_file :83-104, analyse_src
 :120-147) and util/complexity_classification.py (get_difficulty :50-69,
-classify_complexity :72-88, encode_file :134-141) with the same signatures and
-outputs; SI/TI are ADDED (extra "siti" YAML key / extra CSV columns) and the
-existing keys stay byte-identical.  The per-frame SI/TI runs on the MI355X
+classify_complexity :72-88, encode_file :134-141, main :144-247) with the same
+signatures and outputs; SI/TI are ADDED (extra "siti" YAML key / extra `si`,
+`ti` CSV columns) and everything else is byte-identical to the reference's
+output (pinned by tests/golden/src_analysis_fixtures.json).  The per-frame SI/TI runs on the MI355X
 (pp_siti, spec PP-SITI-1) over decoded luma batches; frame ranges of one SRC
 can be split across GPUs with a one-frame halo (``prev``).
 """
@@ -90,18 +91,27 @@ def siti_of_file(videofile, batch=120, reader=None):
     return np.concatenate(sis), np.concatenate(tis)
 
 
-def analyse_src(videofile, ordernum, with_siti=True, src_info=None, stream_sizes=None):
+def siti_yaml_entry(si, ti):
+    """The extra "siti" key of <src>.yaml (spec PP-SITI-1)."""
+    SI, TI = siti_summary(si, ti)
+    return {"si": SI, "ti": TI, "si_frames": [float(v) for v in si],
+            "ti_frames": [None if math.isnan(v) else float(v) for v in ti],
+            "spec": "PP-SITI-1 (ITU-T P.910 Sobel/frame-difference, valid-region SI, ddof=0)"}
+
+
+def analyse_src(videofile, ordernum, with_siti=True, src_info=None, stream_sizes=None, reader=None, siti=None):
     """util/SRC_analysis.py:120-147 plus an extra "siti" key.
 
-    The reference fills get_src_info/get_stream_size by ffprobe
-    (lib/ffmpeg.py:566-633, :399-417); those probes are passed in
-    (``src_info``, ``stream_sizes``) or taken from pixpath.io.probe()."""
+    get_src_info / get_stream_size go through ffprobe exactly as the
+    reference's (pixpath.probe); the keys the reference writes come out
+    byte-identical (tests/test_src_analysis_parity.py).  ``src_info`` /
+    ``stream_sizes`` replace those probes, ``reader`` the decode for SI/TI
+    (pixpath.io reader), ``siti`` precomputed (si_frames, ti_frames)."""
     import yaml
-    from . import io as pio
-    if src_info is None or stream_sizes is None:
-        pr = pio.probe(videofile)
-        src_info = src_info if src_info is not None else pr["stream"]
-        stream_sizes = stream_sizes if stream_sizes is not None else pr["sizes"]
+    from . import probe
+    videoinfo = src_info if src_info is not None else probe.get_src_info(videofile)
+    if stream_sizes is None:
+        stream_sizes = {"v": probe.get_stream_size(videofile), "a": probe.get_stream_size(videofile, "audio")}
     md5filename = videofile + ".md5"
     if not os.path.isfile(md5filename):
         md5hash = str(md5sum(videofile, ordernum).hexdigest())
@@ -109,13 +119,10 @@ def analyse_src(videofile, ordernum, with_siti=True, src_info=None, stream_sizes
         with open(md5filename) as f:
             md5hash = f.readlines()[0].strip().split(" ")[0]
     ret = {"md5sum": md5hash, "get_stream_size": {"v": stream_sizes["v"], "a": stream_sizes["a"]},
-           "get_src_info": src_info}
+           "get_src_info": videoinfo}
     if with_siti:
-        si, ti = siti_of_file(videofile)
-        SI, TI = siti_summary(si, ti)
-        ret["siti"] = {"si": SI, "ti": TI, "si_frames": [float(v) for v in si],
-                       "ti_frames": [None if math.isnan(v) else float(v) for v in ti],
-                       "spec": "PP-SITI-1 (ITU-T P.910 Sobel/frame-difference, valid-region SI, ddof=0)"}
+        si, ti = siti if siti is not None else siti_of_file(videofile, reader=reader)
+        ret["siti"] = siti_yaml_entry(si, ti)
     yaml_path = videofile + ".yaml"
     with open(yaml_path, "w") as outfile:
         yaml.dump(ret, outfile, default_flow_style=False)
@@ -144,9 +151,9 @@ def difficulty_from_info(output_file, info):
 
 
 def get_difficulty(output_file):
-    """util/complexity_classification.py:50-69 (probe through ffprobe)."""
-    from . import io as pio
-    return difficulty_from_info(output_file, pio.segment_info(output_file))
+    """util/complexity_classification.py:50-69 (get_segment_info through ffprobe, pixpath.probe)."""
+    from . import probe
+    return difficulty_from_info(output_file, probe.get_segment_info(output_file))
 
 
 def classify_complexity(complexity, framerate, quantiles):
@@ -173,6 +180,107 @@ def add_siti_columns(rows, siti_by_file):
         r["si"], r["ti"] = si, ti
         out.append(r)
     return out
+
+
+def siti_from_yaml(src_file):
+    """(SI, TI) from <src>.yaml written by analyse_src, or None."""
+    import yaml
+    p = src_file + ".yaml"
+    if not os.path.isfile(p):
+        return None
+    with open(p) as f:
+        d = yaml.safe_load(f) or {}
+    e = d.get("siti")
+    return (float(e["si"]), float(e["ti"])) if e else None
+
+
+def complexity_parse_args(argv=None):
+    """util/complexity_classification.py:91-131, plus --siti {yaml,gpu,none}."""
+    import argparse
+    ap = argparse.ArgumentParser(description="Complexity classification",
+                                 formatter_class=argparse.ArgumentDefaultsHelpFormatter)
+    ap.add_argument("-i", "--input", required=True, nargs="+", help="Input files (SRCs)")
+    ap.add_argument("-t", "--tmp-dir", default=os.path.join(os.getcwd(), "complexityAnalysis"),
+                    help="Path to (temporary) complexity analysis folder")
+    ap.add_argument("-p", "--parallelism", default=1, help="Number of parallel encodes")
+    ap.add_argument("-o", "--output-file", default="complexity_classification.csv", help="Filename of CSV output file")
+    ap.add_argument("-f", "--force", action="store_true", help="Force overwriting (re-analyzing) existing files")
+    ap.add_argument("-v", "--verbose", action="store_true", help="Print debug messages")
+    ap.add_argument("-n", "--dry-run", action="store_true", help="Show what would be run instead of running it")
+    ap.add_argument("--siti", default="yaml", choices=["yaml", "gpu", "none"],
+                    help="si/ti columns: from <src>.yaml (analyse_src), measured on the GPU when absent, or left out")
+    return ap.parse_args(argv)
+
+
+def complexity_main(argv=None):
+    """util/complexity_classification.py:144-247 with `si`, `ti` columns appended
+    (SI/TI of each SRC: its <src>.yaml from analyse_src, else -- with --siti gpu --
+    measured on the MI355X).  Without them the CSV is byte-identical to the
+    reference's (tests/test_src_analysis_parity.py)."""
+    import logging
+    import subprocess
+    import sys
+    from multiprocessing import Pool
+
+    import pandas as pd
+    log = logging.getLogger("main")
+    a = complexity_parse_args(argv)
+    if a.verbose:
+        log.setLevel(logging.DEBUG)
+    if not os.path.isdir(a.tmp_dir):
+        log.info("temporary directory " + str(a.tmp_dir) + " does not exist, creating")
+        os.mkdir(a.tmp_dir)
+    if not a.output_file.endswith(".csv"):
+        log.error("Output file must be .csv!")
+        sys.exit(1)
+    input_files = [f for f in a.input if f.endswith(".avi")]
+    cmds, outputs, src_of = [], [], {}
+    for input_file in input_files:
+        base = os.path.splitext(os.path.basename(input_file))[0]
+        output_file = os.path.join(a.tmp_dir, base + "_crf23.avi")
+        if not (os.path.isfile(output_file) and not a.force):
+            if encode_file(input_file, output_file) not in cmds:  # ParallelRunner keeps a set
+                cmds.append(encode_file(input_file, output_file))
+        outputs.append(output_file)
+        src_of[os.path.basename(output_file)] = input_file
+    if a.dry_run:
+        for c in cmds:
+            log.info(c)
+        sys.exit(0)
+    if cmds:
+        with Pool(int(a.parallelism)) as pool:
+            rcs = pool.map(_shell_rc, cmds)
+        if any(rcs):
+            log.error("There were errors in your commands. Please check the output and re-run the processing chain!")
+            sys.exit(1)
+    all_data = [get_difficulty(o) for o in outputs]
+    if not all_data:
+        log.error("No info calculated, exiting")
+        sys.exit(1)
+    df = pd.DataFrame(all_data)[["file", "norm_bitrate", "complexity", "framerate", "width", "height", "size",
+                                 "duration"]].sort_values("file")
+    quants = {"low": df[df["framerate"] <= 30]["complexity"].quantile([0.25, 0.5, 0.75]),
+              "high": df[df["framerate"] > 30]["complexity"].quantile([0.25, 0.5, 0.75])}
+    df["complexity_class"] = df.apply(lambda x: classify_complexity(x["complexity"], x["framerate"], quants), axis=1)
+    if a.siti != "none":
+        vals = {}
+        for f in df["file"]:
+            src = src_of[f]
+            v = siti_from_yaml(src)
+            if v is None and a.siti == "gpu":
+                v = siti_summary(*siti_of_file(src))
+            vals[f] = v if v is not None else (float("nan"), float("nan"))
+        df["si"] = [vals[f][0] for f in df["file"]]
+        df["ti"] = [vals[f][1] for f in df["file"]]
+    csv_file = os.path.join(a.tmp_dir, a.output_file)
+    log.info("Writing complexity data to " + str(csv_file))
+    df.to_csv(csv_file, index=False)
+    return csv_file
+
+
+def _shell_rc(cmd):
+    import subprocess
+    return subprocess.run(cmd, shell=True).returncode
 
 
 def dump_json(obj, path):
