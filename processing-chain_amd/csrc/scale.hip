@@ -544,7 +544,7 @@ static size_t lds_budget() {
 // tallest chunk whose LDS (staging + ring) fits the budget; ~256-row segments.
 int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::string *err) {
     static const int tws[] = {256, 128, 64, 32};
-    static const int chos[] = {64, 32, 16, 8, 4, 2, 1};
+    static const int chos[] = {64, 48, 32, 24, 16, 8, 4, 2, 1};
     // tuning overrides (measurement only): tallest chunk, rows per segment
     const char *e_cho = std::getenv("PIXPATH_SCALE_CHO_MAX"), *e_seg = std::getenv("PIXPATH_SCALE_SEG_ROWS");
     const int cho_max = e_cho ? std::max(1, atoi(e_cho)) : pp::kChoMax;
