@@ -44,3 +44,35 @@ def smooth_frame(t, fmt, w, h):
 def batch(frames):
     """list of per-frame plane lists -> list of [N, r, c] stacks."""
     return [np.stack([f[p] for f in frames]) for p in range(len(frames[0]))]
+
+
+def extreme_frame(kind, fmt, w, h, seed=0, seams_x=(), seams_y=()):
+    """Full-range test patterns (values 0 and 2^depth - 1, beyond the legal
+    range, as real decodes can carry): they drive swscale's 15-bit clip of the
+    horizontal intermediates and the output clip to [0, max].
+      checker   1-px checkerboard 0/max (the largest filter overshoot)
+      checker4  4-px checkerboard
+      steps     0/max step edges at the given source columns / rows (strip and
+                segment seams), alternating
+      noise     uniform noise over the full range [0, max]"""
+    depth, hs, vs = po.fmt_info(fmt)
+    dt = np.uint16 if depth > 8 else np.uint8
+    mx = (1 << depth) - 1
+    rng = np.random.default_rng(seed)
+    out = []
+    for p, (r, c) in enumerate(po.plane_shapes(fmt, w, h)):
+        yy, xx = np.mgrid[0:r, 0:c]
+        if kind == "checker":
+            v = ((yy + xx + p) & 1) * mx
+        elif kind == "checker4":
+            v = (((yy >> 2) + (xx >> 2) + p) & 1) * mx
+        elif kind == "steps":
+            sx = np.searchsorted(np.asarray(sorted(int(x) >> (hs if p else 0) for x in seams_x)), xx, side="right")
+            sy = np.searchsorted(np.asarray(sorted(int(y) >> (vs if p else 0) for y in seams_y)), yy, side="right")
+            v = ((sx + sy + p) & 1) * mx
+        elif kind == "noise":
+            v = rng.integers(0, mx + 1, (r, c))
+        else:
+            raise ValueError(kind)
+        out.append(v.astype(dt))
+    return out

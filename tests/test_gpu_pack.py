@@ -79,12 +79,18 @@ def test_stall_compose_matches_oracle(gpu, fmt):
     (po.YUV422P10LE, 1920, 1080, 1920, 1080), (po.YUV422P10LE, 1280, 534, 1280, 720), (po.YUV420P10LE, 100, 38, 100, 50),
     (po.YUV420P, 102, 38, 102, 50),
 ])
-def test_fused_cpvs_matches_chain(gpu, fmt, w, h, W, H):
-    """pp_cpvs_execute == pad -> swscale (bicubic, -> uyvy422 / yuv422p10le) -> v210, bit-exact."""
+@pytest.mark.parametrize("content", ["legal", "checker", "noise"])
+def test_fused_cpvs_matches_chain(gpu, fmt, w, h, W, H, content):
+    """pp_cpvs_execute == pad -> swscale (bicubic, -> uyvy422 / yuv422p10le) -> v210, bit-exact;
+    legal-range noise, and full-range 0/max checkerboards and noise (the 4:2:0 ->
+    4:2:2 vertical filter's clip and v210's [4, 1019] clip)."""
     from pixpath import ops
     from pixpath.frames import FrameBatch
     rng = np.random.default_rng(8)
-    frames = [synth.noise_frame(rng, fmt, w, h) for _ in range(2)]
+    if content == "legal":
+        frames = [synth.noise_frame(rng, fmt, w, h) for _ in range(2)]
+    else:
+        frames = [synth.extreme_frame(content, fmt, w, h, seed=i) for i in range(2)]
     src = FrameBatch.from_numpy(fmt, synth.batch(frames), device=gpu)
     out = ops.cpvs(src, W, H).to_numpy()[0]
     depth = po.fmt_info(fmt)[0]
