@@ -33,6 +33,7 @@ extern "C" int pp_ctx_create(int device, pp_ctx **out) {
         PP_FAIL(PP_ERR_UNSUPPORTED, "libpixpath is built for gfx950, device %d is %s", device, prop.gcnArchName);
     pp_ctx *c = new pp_ctx();
     c->device = device;
+    c->cus = prop.multiProcessorCount;
     *out = c;
     return PP_OK;
 }

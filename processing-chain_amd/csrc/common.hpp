@@ -69,6 +69,7 @@ __host__ __device__ inline int xcd_remap(int b, int n) {
 
 struct Ctx {
     int device = 0;
+    int cus = 0;  // compute units (persistent grids)
     // spinner animation (PP-STALL-1), device resident
     int spin_fmt = -1, spin_n = 0, spin_w = 0, spin_h = 0;
     void *spin_buf = nullptr; // [n][Y(w*h) A(w*h) U V Ac (cw*ch each)] uint16

@@ -226,3 +226,33 @@ def fps_index_map(n_in, in_rate, out_rate):
             i += 1
         out.append(i)
     return out
+
+
+def _round_near(num, den):
+    """av_rescale_rnd(..., AV_ROUND_NEAR_INF) for non-negative num / den."""
+    return (2 * num + den) // (2 * den)
+
+
+def select_fps_map(n_in, in_rate, out_rate, select_expr=""):
+    """`select='expr',fps=fps=F` over n_in input frames at in_rate (row a14):
+    the input frame shown at each output frame.
+
+    select keeps frame n when the expression is non-zero and leaves its
+    timestamp n / in_rate unchanged; vf_fps (libavfilter/vf_fps.c, rounding
+    =near) converts each kept frame's timestamp to output frame units, starts
+    at the first one, shows the newest kept frame whose converted timestamp is
+    <= the output frame's, and stops at the end-of-stream timestamp
+    n_in / in_rate.  Without a select this is fps_index_map."""
+    a, b = Fraction(in_rate), Fraction(out_rate)
+    N, D = a.denominator * b.numerator, a.numerator * b.denominator  # t_out = n * N / D
+    kept = [n for n in range(n_in) if eval_select(select_expr, n)]
+    if not kept:
+        return []
+    q = [_round_near(n * N, D) for n in kept]
+    q_eof = _round_near(n_in * N, D)
+    out, i = [], 0
+    for j in range(q[0], q_eof):
+        while i + 1 < len(q) and q[i + 1] <= j:
+            i += 1
+        out.append(kept[i])
+    return out

@@ -2,6 +2,8 @@
 builders return (same positional output file, -y/-n overwrite convention as
 the ffmpeg strings they replace).
 
+  encseg p01 encode_segment: trimmed decode -> scale=W:-2 (+ -pix_fmt) -> select/fps -> Y4M
+         for the encoder (lib/ffmpeg.py:772-937)
   avpvs  decode -> scale (+ -pix_fmt conversion) [-> fps] [-> long-test canvas] -> encode
          (create_avpvs_short lib/ffmpeg.py:940, create_avpvs_segment :1003)
   cpvs   decode AVPVS -> fps -> [pad] -> uyvy422 / v210 packing -> encode
@@ -129,6 +131,41 @@ def cmd_avpvs(args):
         while wr.n < cap:  # overlay eof_action=repeat: the canvas keeps the last frame
             wr.write(wr.last)
     rd.close()
+    wr.close()
+    return 0
+
+
+def cmd_encseg(args):
+    """p01 encode_segment's pixel work (lib/ffmpeg.py:794-837): trimmed decode,
+    `scale=W:-2:flags=bicubic` (+ the encoder's -pix_fmt conversion) on the
+    MI355X, `select` + `fps` as a host frame map; Y4M out (a path or - for
+    stdout) for the reference's encoder invocation."""
+    import torch
+    from . import chain, formats, io as pio, ops
+    from .pipeline import Pipeline, Stage
+    dev = _device()
+    torch.cuda.set_device(dev)
+    rd = pio.open_reader(args.input, start=args.start, duration=args.duration)
+    W = int(args.width)
+    H = chain.scale_height_keep_aspect(rd.w, rd.h, W)
+    target = formats.fmt(args.pix_fmt)
+    in_rate = Fraction(args.in_fps) if args.in_fps else Fraction(rd.rate)
+    out_rate = Fraction(str(args.fps))
+    # frames the trimmed decode yields: the -t window at the input rate
+    n_in = int(round(Fraction(str(args.duration)) * in_rate)) if args.duration else None
+    if n_in is None:
+        raise SystemExit("pixpath encseg: --duration is required")
+    fmap = chain.select_fps_map(n_in, in_rate, out_rate, args.select or "")
+    keep = sorted(set(fmap))
+    counts = {k: 0 for k in keep}
+    for k in fmap:
+        counts[k] += 1
+    sel = pio.SelectReader(rd, keep)
+    sc = ops.Scaler(rd.fmt, rd.w, rd.h, target, W, H, flags=args.flags)
+    stage = Stage(rd.fmt, rd.w, rd.h, target, W, H, lambda s, d, st: sc(s, d, stream=st))
+    wr = pio.Y4MWriter(args.output, target, W, H, out_rate)
+    Pipeline(stage, batch=args.batch, device=dev).run(sel, wr, emit=lambda i: counts[keep[i]])
+    sel.close()
     wr.close()
     return 0
 
@@ -345,6 +382,20 @@ def main(argv=None):
     p.add_argument("--duration", default=None)
     p.add_argument("--overlay-yuv420", action="store_true")
     p.set_defaults(fn=cmd_avpvs)
+
+    p = sub.add_parser("encseg")
+    p.add_argument("--input", required=True)
+    p.add_argument("--batch", type=int, default=32)
+    p.add_argument("--start", default=None)
+    p.add_argument("--duration", default=None)
+    p.add_argument("--width", required=True)
+    p.add_argument("--flags", default="bicubic")
+    p.add_argument("--pix-fmt", required=True)
+    p.add_argument("--select", default="")
+    p.add_argument("--fps", required=True)
+    p.add_argument("--in-fps", default=None)
+    p.add_argument("output")
+    p.set_defaults(fn=cmd_encseg)
 
     p = sub.add_parser("cpvs")
     common(p)

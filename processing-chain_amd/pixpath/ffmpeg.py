@@ -17,6 +17,7 @@ PIXPATH_BACKEND:
 
 Reference functions mirrored (file:line in pnats2avhd/processing-chain):
   calculate_avpvs_video_dimensions  lib/ffmpeg.py:33
+  encode_segment                    lib/ffmpeg.py:772 (p01; the encoder options stay the reference's)
   create_avpvs_short                lib/ffmpeg.py:940
   create_avpvs_segment              lib/ffmpeg.py:1003
   create_avpvs_long_concat          lib/ffmpeg.py:1058
@@ -29,6 +30,7 @@ Reference functions mirrored (file:line in pnats2avhd/processing-chain):
 import logging
 import os
 import shlex
+import sys
 
 from .chain import calculate_avpvs_video_dimensions  # noqa: F401  (re-export, a1)
 from .chain import buffer_string, encode_segment_filter_chain  # noqa: F401
@@ -71,6 +73,123 @@ def _gpu_cli(sub, args):
                                                                 " ".join(shlex.quote(str(a)) for a in args))
 
 
+def encode_segment(segment, overwrite=False, video_encoder_command=None):
+    """p01 segment encode (lib/ffmpeg.py:772-937): `-ss/-t` trim, then
+    `scale=W:-2:flags=bicubic[,select='...'],fps=fps=F`, then the encoder.
+
+    ``video_encoder_command(segment, current_pass=1, total_passes=1, logfile="")``
+    is the reference's own _get_video_encoder_command (lib/ffmpeg.py:61-318):
+    encoders are not part of the pixel path, so the drop-in takes it from the
+    reference module.  In the ffmpeg backend the
+    string is the reference's byte for byte.  In the gpu backend
+    ``pixpath.cli encseg`` decodes the trimmed range, runs scale (+ the
+    -pix_fmt conversion) on the MI355X and the select/fps frame choice on the
+    host (pixpath.chain.select_fps_map), and hands the frames to the same
+    encoder invocation(s) as Y4M (two-pass encodes read a temporary Y4M twice).
+    """
+    if video_encoder_command is None:
+        raise TypeError("encode_segment needs the reference's _get_video_encoder_command "
+                        "(video_encoder_command=...)")
+    from fractions import Fraction
+
+    from .chain import get_fps, select_expression
+    test_config = segment.src.test_config
+    input_file = segment.src.file_path
+    output_file = os.path.join(test_config.get_video_segments_path(), segment.get_filename())
+    if overwrite:
+        overwrite_spec = "-y"
+    else:
+        overwrite_spec = "-n"
+        if os.path.isfile(output_file):
+            logger.warning("output " + output_file + " already exists, will not convert. Use --force to force overwriting.")
+            return None
+    nr_threads_opt = "" if segment.quality_level.video_codec == "av1" else " -threads 1"
+    filters = encode_segment_filter_chain(segment)
+    if test_config.type == "long":
+        audio_encoder_cmd = "-c:a {} -b:a {}k".format(segment.audio_coding.encoder, segment.quality_level.audio_bitrate)
+    else:
+        audio_encoder_cmd = ""
+    passes = segment.video_coding.passes
+    if passes not in (1, 2) and not (segment.video_coding.crf or segment.video_coding.qp):
+        logger.error("only 1 or 2 pass or crf encoding implemented")
+        sys.exit(1)
+
+    if _backend == "gpu":
+        fps_cmd, fps = get_fps(segment)
+        orig_fps = float(Fraction(segment.src.stream_info["r_frame_rate"]))
+        sel = select_expression(orig_fps, fps) if fps_cmd else ""
+        out_fps = fps if fps_cmd else orig_fps
+        tmp = os.path.join(test_config.get_video_segments_path(),
+                           ".pixpath_" + os.path.splitext(os.path.basename(output_file))[0] + ".y4m")
+        dec = _gpu_cli("encseg", ["--input", input_file, "--start", segment.start_time, "--duration",
+                                  segment.duration, "--width", segment.quality_level.width, "--flags", "bicubic",
+                                  "--pix-fmt", segment.target_pix_fmt, "--select", sel, "--fps", out_fps,
+                                  "--in-fps", segment.src.stream_info["r_frame_rate"], tmp if passes == 2 else "-"])
+        # audio (long tests) from the trimmed SRC as in the reference command
+        audio_in = ("-ss {} -t {} -i {} -map 0:v -map 1:a".format(segment.start_time, segment.duration, input_file)
+                    if audio_encoder_cmd else "")
+        if passes == 2:
+            passlogfile = os.path.join(test_config.get_logs_path(),
+                                       "passlogfile_" + os.path.splitext(os.path.basename(output_file))[0])
+            output_format = {"mp4": "mp4", "mkv": "matroska"}.get(segment.ext)
+            if output_format is None:
+                logger.error("unknown segment extension " + segment.ext)
+            common = "-nostdin -f yuv4mpegpipe -i {} {} -video_track_timescale 90000 {}".format(
+                tmp, audio_in, audio_encoder_cmd)
+            cmd = " ".join([dec, "&&", "ffmpeg -y", common,
+                            video_encoder_command(segment, current_pass=1, total_passes=2, logfile=passlogfile),
+                            "-f", str(output_format), "/dev/null", "&&", "ffmpeg", overwrite_spec, common,
+                            video_encoder_command(segment, current_pass=2, total_passes=2, logfile=passlogfile),
+                            output_file, ";", "rc=$?; rm -f", tmp, "; exit $rc"])
+        else:
+            cmd = " ".join([dec, "|", "ffmpeg -nostdin", overwrite_spec, "-f yuv4mpegpipe -i -", audio_in,
+                            "-video_track_timescale 90000", video_encoder_command(segment), audio_encoder_cmd,
+                            output_file])
+        return _collapse(cmd)
+
+    common_fmt = """
+        -nostdin
+        -ss {start} -i {input_file}
+        {nr_threads_opt}
+        -t {dur}
+        -video_track_timescale 90000
+        -filter:v {filters}
+        {audio_encoder_cmd}
+        """
+    if passes == 2:
+        common_opts = common_fmt.format(start=segment.start_time, dur=segment.duration, **locals())
+        passlogfile = os.path.join(test_config.get_logs_path(),
+                                   "passlogfile_" + os.path.splitext(os.path.basename(output_file))[0])
+        if segment.ext == "mp4":
+            output_format = "mp4"
+        elif segment.ext == "mkv":
+            output_format = "matroska"
+        else:
+            logger.error("unknown segment extension " + segment.ext)
+        pass1 = " ".join(["ffmpeg", "-y", common_opts,
+                          video_encoder_command(segment, current_pass=1, total_passes=2, logfile=passlogfile),
+                          "-f", output_format, "/dev/null"])
+        pass2 = " ".join(["ffmpeg", overwrite_spec, common_opts,
+                          video_encoder_command(segment, current_pass=2, total_passes=2, logfile=passlogfile),
+                          output_file])
+        cmd = pass1 + " && " + pass2
+    else:  # one pass, or crf/qp
+        cmd = """
+        ffmpeg -nostdin
+        {overwrite_spec}
+        -ss {start} -i {input_file}
+        {nr_threads_opt}
+        -t {dur}
+        -video_track_timescale 90000
+        -filter:v {filters}
+        {video_encoder_cmd}
+        {audio_encoder_cmd}
+        {output_file}
+        """.format(start=segment.start_time, dur=segment.duration, video_encoder_cmd=video_encoder_command(segment),
+                   **locals())
+    return _collapse(cmd)
+
+
 def create_avpvs_short(pvs, overwrite=False, scale_avpvs_tosource=False, force_60_fps=False, post_proc_id=0):
     """Decode the first segment, upscale to the AVPVS size, FFV1 + FLAC (lib/ffmpeg.py:940-1000)."""
     test_config = pvs.test_config
@@ -101,8 +220,11 @@ def create_avpvs_short(pvs, overwrite=False, scale_avpvs_tosource=False, force_6
     if _backend == "gpu":
         args = [overwrite_spec, "--input", input_file, "--size", "%dx%d" % (w, h), "--flags", "bicubic",
                 "--pix-fmt", target_pix_fmt, "--vopts", FFV1_OPTS, "--aopts", "-c:a flac"]
-        if fps is not None:  # the GPU path applies the fps the reference intended
-            args += ["--fps", fps]
+        if fps is not None:
+            # the reference passes the unexpanded placeholder `fps={src_framerate}`
+            # to ffmpeg, which rejects it and the run fails (lib/ffmpeg.py:958-961);
+            # the GPU backend hands over the same literal and fails the same way
+            args += ["--fps", "{src_framerate}"]
         return _collapse(_gpu_cli("avpvs", args + [output_file]))
 
     cmd = """

@@ -125,13 +125,17 @@ class RawReader(Reader):
 
 
 class FFmpegReader(RawReader):  # pragma: no cover - needs ffmpeg
-    """Decode any container through `ffmpeg ... -f rawvideo -pix_fmt F pipe:1`."""
+    """Decode any container through `ffmpeg ... -f rawvideo -pix_fmt F pipe:1`
+    (optionally trimmed like the reference's p01 encode: `-ss S -i IN -t D`)."""
 
-    def __init__(self, path, f=None, w=None, h=None, rate=None):
+    def __init__(self, path, f=None, w=None, h=None, rate=None, start=None, duration=None):
         st = probe(path)["stream"]
         f = f or st["pix_fmt"]
-        self.proc = subprocess.Popen(["ffmpeg", "-nostdin", "-v", "error", "-i", path, "-f", "rawvideo",
-                                      "-pix_fmt", f, "pipe:1"], stdout=subprocess.PIPE, bufsize=1 << 24)
+        pre = ["-ss", str(start)] if start is not None else []
+        post = ["-t", str(duration)] if duration is not None else []
+        self.proc = subprocess.Popen(["ffmpeg", "-nostdin", "-v", "error"] + pre + ["-i", path] + post +
+                                     ["-f", "rawvideo", "-pix_fmt", f, "pipe:1"], stdout=subprocess.PIPE,
+                                     bufsize=1 << 24)
         super().__init__(self.proc.stdout, f, w or st["width"], h or st["height"],
                          rate or Fraction(st["r_frame_rate"]))
 
@@ -152,7 +156,8 @@ class Writer:
 
 class Y4MWriter(Writer):
     def __init__(self, path, f, w, h, rate=60):
-        self.fh = open(path, "wb")
+        import sys
+        self.fh = sys.stdout.buffer if path == "-" else open(path, "wb")
         r = Fraction(rate)
         self.fb = formats.frame_bytes(f, w, h)
         self.fh.write(("YUV4MPEG2 W%d H%d F%d:%d Ip A1:1 C%s\n" % (w, h, r.numerator, r.denominator,
@@ -202,13 +207,68 @@ class FFmpegWriter(Writer):  # pragma: no cover - needs ffmpeg
             raise RuntimeError("ffmpeg encode failed")
 
 
-def open_reader(path, f=None, w=None, h=None, rate=None):
+class TrimmedReader(Reader):
+    """Frames [skip, skip + count) of another reader (input seeking -ss / -t on
+    files read directly; exact when the times are whole frame periods)."""
+
+    def __init__(self, inner, skip, count=None):
+        self.inner, self.left = inner, count
+        self.fmt, self.w, self.h, self.rate = inner.fmt, inner.w, inner.h, inner.rate
+        if skip:
+            buf = bytearray(inner.frame_bytes)
+            for _ in range(skip):
+                if not inner._read_frame(memoryview(buf)):
+                    break
+
+    def _read_frame(self, mv):
+        if self.left is not None:
+            if self.left <= 0:
+                return False
+            self.left -= 1
+        return self.inner._read_frame(mv)
+
+    def close(self):
+        self.inner.close()
+
+
+class SelectReader(Reader):
+    """Only the input frames whose index is in `keep` (a sorted list): frames a
+    select/fps map drops are never sent to the GPU."""
+
+    def __init__(self, inner, keep):
+        self.inner, self.keep, self.i, self.k = inner, keep, 0, 0
+        self.fmt, self.w, self.h, self.rate = inner.fmt, inner.w, inner.h, inner.rate
+        self._skip = bytearray(inner.frame_bytes)
+
+    def _read_frame(self, mv):
+        if self.k >= len(self.keep):
+            return False
+        while self.i < self.keep[self.k]:
+            if not self.inner._read_frame(memoryview(self._skip)):
+                return False
+            self.i += 1
+        ok = self.inner._read_frame(mv)
+        self.i += 1
+        self.k += 1
+        return ok
+
+    def close(self):
+        self.inner.close()
+
+
+def open_reader(path, f=None, w=None, h=None, rate=None, start=None, duration=None):
+    """Reader for a Y4M / raw file (read directly) or any container (ffmpeg
+    decode pipe); start/duration trim like `-ss start -i path -t duration`."""
     ext = os.path.splitext(path)[1].lower()
-    if ext == ".y4m":
-        return Y4MReader(path)
-    if ext in (".raw", ".yuv"):
-        return RawReader(path, f, w, h, rate or 60)
-    return FFmpegReader(path, f, w, h, rate)
+    if ext in (".y4m", ".raw", ".yuv"):
+        rd = Y4MReader(path) if ext == ".y4m" else RawReader(path, f, w, h, rate or 60)
+        if start is None and duration is None:
+            return rd
+        r = Fraction(rd.rate)
+        skip = int(round(Fraction(str(start or 0)) * r))
+        count = None if duration is None else int(round(Fraction(str(duration)) * r))
+        return TrimmedReader(rd, skip, count)
+    return FFmpegReader(path, f, w, h, rate, start=start, duration=duration)
 
 
 def probe(path):

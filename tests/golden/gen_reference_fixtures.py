@@ -115,7 +115,10 @@ def main():
             res = rff.encode_segment(scenarios.encode_segment_stub(sc), overwrite=True)
         except SystemExit as e:
             res = {"sys_exit": e.code}
-        enc.append([sc, res])
+        # the encoder options (not pixel work): what the drop-in receives from
+        # the reference's _get_video_encoder_command
+        venc = call(rff._get_video_encoder_command, scenarios.encode_segment_stub(sc))
+        enc.append([sc, res, venc])
     out["encode_segment"] = enc
 
     # command builders

@@ -126,3 +126,34 @@ def test_cli_siti(gpu, tmp_path, capsys):
     np.testing.assert_allclose(res["si_frames"], rsi, rtol=1e-4)
     np.testing.assert_allclose(res["ti_frames"][1:], rti[1:], rtol=1e-9)
     assert res["ti_frames"][0] is None and abs(res["si"] - rsi.max()) <= 1e-4 * rsi.max()
+
+
+@pytest.mark.parametrize("in_fps,out_fps,n,start,dur", [
+    (60, 30, 40, "0.1", "0.5"),      # mod(n+1,2)
+    (24, 15, 40, "0.25", "1.25"),    # the 62.5 % select pattern
+    (60, 60, 20, "0", "0.2"),        # no select: fps=fps=orig
+])
+def test_cli_encseg_trim_scale_select_fps(gpu, tmp_path, in_fps, out_fps, n, start, dur):
+    """p01 encode_segment, gpu backend (pixpath.cli encseg): -ss/-t trim, scale=W:-2:flags=bicubic
+    (+ -pix_fmt yuv420p) on the GPU, select + fps on the host; every output frame vs the oracle."""
+    from fractions import Fraction
+
+    from pixpath import cli
+    rng = np.random.default_rng(3)
+    frames = [synth.noise_frame(rng, po.YUV422P10LE, 384, 216) for _ in range(n)]
+    src, out = str(tmp_path / "src.y4m"), str(tmp_path / "enc.y4m")
+    _write_y4m(src, "yuv422p10le", frames, 384, 216, rate=in_fps)
+    sel = chain.select_expression(float(in_fps), float(out_fps)) if in_fps != out_fps else ""
+    assert cli.main(["encseg", "--input", src, "--start", start, "--duration", dur, "--width", "256",
+                     "--pix-fmt", "yuv420p", "--select", sel, "--fps", str(out_fps), "--in-fps", str(in_fps),
+                     "--batch", "8", out]) == 0
+    got = _read(out)
+    h = chain.scale_height_keep_aspect(384, 216, 256)
+    skip = int(round(Fraction(start) * in_fps))
+    n_in = int(round(Fraction(dur) * in_fps))
+    m = chain.select_fps_map(n_in, in_fps, out_fps, sel)
+    assert got[0].shape == (len(m), h, 256)
+    for j, k in enumerate(m):
+        ref = po.scale(po.YUV422P10LE, frames[skip + k], po.YUV420P, 256, h, po.SWS_BICUBIC)
+        for p in range(3):
+            np.testing.assert_array_equal(got[p][j], ref[p], err_msg="out %d <- in %d plane %d" % (j, skip + k, p))

@@ -98,5 +98,5 @@ def test_full_range_extremes(gpu, plan, kind, kernel, monkeypatch):
                 bad = np.argwhere(out[p][i] != r)
                 pytest.fail("frame %d plane %d: %d mismatches, first at %s got %d want %d" % (
                     i, p, len(bad), tuple(bad[0]), out[p][i][tuple(bad[0])], r[tuple(bad[0])]))
-    if kind in ("checker", "steps"):
+    if kind == "steps" or (kind == "checker" and dw >= sw):  # a downscale averages a 1-px checker to grey
         assert hit_clip, "pattern did not reach the output clip"

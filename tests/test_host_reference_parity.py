@@ -76,11 +76,45 @@ def test_get_fps(args, want):
     assert (r if isinstance(r, dict) else list(r)) == want
 
 
-@pytest.mark.parametrize("sc,want", FX["encode_segment"])
-def test_encode_segment_filter_chain(sc, want):
+@pytest.mark.parametrize("sc,want,venc", FX["encode_segment"])
+def test_encode_segment_filter_chain(sc, want, venc):
     seg = scenarios.encode_segment_stub(sc)
     chain_str = chain.encode_segment_filter_chain(seg)
     assert ("-filter:v " + chain_str + " ") in want
+
+
+@pytest.mark.parametrize("sc,want,venc", FX["encode_segment"])
+def test_encode_segment_ffmpeg_backend_identical(sc, want, venc):
+    """pixpath.ffmpeg.encode_segment == the reference's string, with the
+    reference's own encoder options (what lib/ffmpeg.py hands the drop-in)."""
+    pff.set_backend("ffmpeg")
+    got = pff.encode_segment(scenarios.encode_segment_stub(sc), overwrite=True,
+                             video_encoder_command=lambda seg, **kw: venc)
+    assert got == want
+
+
+@pytest.mark.parametrize("sc,want,venc", FX["encode_segment"])
+def test_encode_segment_gpu_backend(sc, want, venc):
+    """GPU backend: decode + trim + scale on the MI355X + select/fps on the host
+    in `pixpath.cli encseg`, then the reference's encoder options on Y4M."""
+    import shlex
+    pff.set_backend("gpu")
+    try:
+        got = pff.encode_segment(scenarios.encode_segment_stub(sc), overwrite=True,
+                                 video_encoder_command=lambda seg, **kw: venc)
+    finally:
+        pff.set_backend("ffmpeg")
+    dec, enc = got.split(" | ")
+    a = shlex.split(dec)
+    assert a[a.index("--width") + 1] == str(sc["ql"][0]) and a[a.index("--pix-fmt") + 1] == sc["pix"]
+    assert a[a.index("--in-fps") + 1] == str(sc["src_fps"]) and a[-1] == "-"
+    seg = scenarios.encode_segment_stub(sc)
+    fps_cmd, fps = chain.get_fps(seg)
+    sel = chain.select_expression(float(sc["src_fps"]), fps) if fps_cmd else ""
+    assert a[a.index("--select") + 1] == sel
+    assert float(a[a.index("--fps") + 1]) == float(fps if fps_cmd else sc["src_fps"])
+    assert enc.startswith("ffmpeg -nostdin -y -f yuv4mpegpipe -i - -video_track_timescale 90000 ")
+    assert " ".join(venc.split()) in enc and enc.endswith(seg.get_filename())
 
 
 @pytest.mark.parametrize("i", range(len(FX["builders"])))
