@@ -241,99 +241,70 @@ def cmd_cpvs(args):
     return 0
 
 
-def stall_schedule(buffer_events, rate, n_in, skipping, spinner_delays=None, black_frame=True):
-    """PP-STALL-1 output sequence for an AVPVS of n_in frames at `rate`.
-
-    Returns a list of (src_index, spinner_index): src_index -1 = black frame,
-    spinner_index -1 = no overlay.  Stalls ([media_t, dur]) insert round(dur*rate)
-    frames after frame round(media_t*rate)-1 showing that frame (black when the
-    stall is at t=0 and black_frame is set) with the spinner animated at its own
-    frame delays; freezes ([t, dur], skipping) replace the frames of [t, t+dur)
-    by the frame before t, keeping the length."""
-    rate = Fraction(rate)
-    seq = [(i, -1) for i in range(n_in)]
-    if skipping:
-        for t, d in sorted(buffer_events):
-            a = int(round(t * rate))
-            b = min(n_in, int(round((t + d) * rate)))
-            for i in range(a, b):
-                seq[i] = (max(a - 1, 0), -1)
-        return seq
-    # exact rational clock: APNG delays are num/den fractions
-    delays = [Fraction(float(d)).limit_denominator(100000) for d in
-              (spinner_delays if spinner_delays is not None else [0.0])]
-    period = sum(delays)
-    out, cursor = [], 0
-    for t, d in sorted(buffer_events):
-        at = min(n_in, int(round(t * rate)))
-        out.extend(seq[cursor:at])
-        cursor = at
-        frozen = at - 1 if at > 0 else (-1 if black_frame else 0)
-        k = int(round(d * rate))
-        for j in range(k):
-            ts = (Fraction(j) / rate) % period if period > 0 else Fraction(0)
-            acc, si = Fraction(0), 0
-            for si, dl in enumerate(delays):
-                acc += dl
-                if ts < acc:
-                    break
-            out.append((frozen, si))
-    out.extend(seq[cursor:])
-    return out
+from .stall import stall_schedule  # noqa: E402,F401  (PP-STALL-1, re-exported for callers/tests)
 
 
 def cmd_stall(args):
+    """bufferer replacement (p03_generateAvPvs.py:236-243, spec PP-STALL-1):
+    the AVPVS is read once, in order; input frames pass through untouched,
+    stall runs are composed on the GPU from the one retained frame (frozen
+    frame or black + spinner), and the audio gets the stalls' silence."""
     import torch
-    from . import formats, io as pio, ops, spinner
+    from . import io as pio, ops, spinner
     from .frames import FrameBatch
+    from .stall import StallStream, stall_audio_graph, stall_times
     out = args.output
     if _skip(out, args.y):
         return 0
     dev = _device()
     torch.cuda.set_device(dev)
+    device = torch.device("cuda", dev)
     rd = pio.open_reader(args.input)
-    fmt = rd.fmt
+    fmt, w, h = rd.fmt, rd.w, rd.h
     events = ast.literal_eval(args.buffer)
-    fb = rd.frame_bytes
-    # the AVPVS is decoded once into host memory (the stall schedule indexes it)
-    frames = []
-    while True:
-        buf = np.empty((64, fb), np.uint8)
-        k = rd.read_into(buf, 64)
-        if k:
-            frames.append(buf[:k])
-        if k < 64:
-            break
-    allf = np.concatenate(frames) if frames else np.empty((0, fb), np.uint8)
-    n_in = allf.shape[0]
     delays = None
     if not args.skipping:
         anim, delays = spinner.load_apng(args.spinner)
         ops.spinner_upload(anim, fmt, device=dev)
-    seq = stall_schedule(events, rd.rate, n_in, args.skipping, delays, black_frame=args.black_frame)
-    wr = _open_writer(out, fmt, rd.w, rd.h, rd.rate, args.vopts, args.aopts, None, args.y)
-    # frames without overlay pass through untouched; stall frames are composed on the GPU in batches
-    i = 0
-    while i < len(seq):
-        s, sp = seq[i]
-        if sp < 0:
-            wr.write(allf[s] if s >= 0 else _black(fmt, rd.w, rd.h))
-            i += 1
-            continue
-        j = i
-        while j < len(seq) and seq[j][1] >= 0 and j - i < 256:
-            j += 1
-        block = seq[i:j]
-        srcs = sorted({b[0] for b in block if b[0] >= 0})
-        remap = {s_: k for k, s_ in enumerate(srcs)}
-        src_b = FrameBatch.interleaved(fmt, rd.w, rd.h, max(1, len(srcs)), device=torch.device("cuda", dev))
-        if srcs:
-            src_b.storage.copy_(torch.from_numpy(allf[srcs]).to(src_b.storage.device))
-        dst_b = FrameBatch.interleaved(fmt, rd.w, rd.h, len(block), device=torch.device("cuda", dev))
-        ops.stall_compose(src_b, [remap.get(b[0], -1) if b[0] >= 0 else -1 for b in block],
-                          [b[1] for b in block], dst=dst_b)
-        wr.write(dst_b.storage.cpu().numpy())
-        i = j
+    audio_from, graph = None, None
+    if args.aopts.strip() != "-an" and os.path.splitext(out)[1].lower() not in (".y4m", ".raw", ".yuv"):
+        ap = pio.audio_params(args.input)  # pragma: no cover - needs ffprobe
+        if ap is not None:
+            audio_from = args.input
+            if not args.skipping:
+                graph = stall_audio_graph(stall_times(events, rd.rate), ap[0], ap[1])
+    if audio_from:  # pragma: no cover - needs ffmpeg
+        wr = pio.FFmpegWriter(out, fmt, w, h, rd.rate, args.vopts, args.aopts, audio_from=audio_from,
+                              overwrite="-y" if args.y else "-n", audio_filter=graph)
+    else:
+        wr = _open_writer(out, fmt, w, h, rd.rate, args.vopts, args.aopts, None, args.y)
+    fb = rd.frame_bytes
+    src_b = FrameBatch.interleaved(fmt, w, h, 1, device=device)
+    blk = 256
+    dst_b = FrameBatch.interleaved(fmt, w, h, blk, device=device)
+    host = torch.empty((blk, fb), dtype=torch.uint8).pin_memory()
+
+    def frames():
+        buf = np.empty((1, fb), np.uint8)
+        while rd.read_into(buf, 1) == 1:
+            yield buf[0].copy()
+
+    def emit_input(f):
+        wr.write(f)
+
+    def emit_stall(f, spin):
+        if f is not None:
+            src_b.storage.copy_(torch.from_numpy(f).view(1, fb).to(device, non_blocking=False))
+        for i in range(0, len(spin), blk):
+            part = spin[i:i + blk]
+            n = len(part)
+            ops.stall_compose(src_b, [0 if f is not None else -1] * n, part,
+                              dst=FrameBatch.interleaved(fmt, w, h, n, device=device, storage=dst_b.storage[:n]))
+            host[:n].copy_(dst_b.storage[:n])  # synchronous D2H into pinned memory
+            wr.write(host[:n].numpy())
+
+    StallStream(events, rd.rate, args.skipping, delays, black_frame=args.black_frame).run(
+        frames(), emit_input, emit_stall)
     rd.close()
     wr.close()
     return 0

@@ -187,13 +187,17 @@ class RawWriter(Writer):
 class FFmpegWriter(Writer):  # pragma: no cover - needs ffmpeg
     """Encode raw frames with the reference's encoder options (e.g. FFV1 / v210 / rawvideo)."""
 
-    def __init__(self, path, f, w, h, rate, vopts, aopts="-an", audio_from=None, overwrite="-y", extra_in=""):
+    def __init__(self, path, f, w, h, rate, vopts, aopts="-an", audio_from=None, overwrite="-y", extra_in="",
+                 audio_filter=None):
         r = Fraction(rate)
         cmd = "ffmpeg -nostdin -v error {ow} -f rawvideo -pix_fmt {pf} -s {w}x{h} -r {num}/{den} -i pipe:0 ".format(
             ow=overwrite, pf=formats.fmt(f).name if not formats.fmt(f).packed else
             ("uyvy422" if formats.fmt(f).id == formats.UYVY422 else "yuv422p10le"),
             w=w, h=h, num=r.numerator, den=r.denominator)
-        if audio_from:
+        if audio_from and audio_filter:
+            cmd += "-i {} -filter_complex {} -map 0:v -map '[aout]' ".format(shlex.quote(audio_from),
+                                                                          shlex.quote(audio_filter))
+        elif audio_from:
             cmd += "-i {} -map 0:v -map 1:a? ".format(shlex.quote(audio_from))
         cmd += "{} {} {} {}".format(extra_in, vopts, aopts, shlex.quote(path))
         self.proc = subprocess.Popen(cmd, shell=True, stdin=subprocess.PIPE, bufsize=1 << 24)
@@ -269,6 +273,19 @@ def open_reader(path, f=None, w=None, h=None, rate=None, start=None, duration=No
         count = None if duration is None else int(round(Fraction(str(duration)) * r))
         return TrimmedReader(rd, skip, count)
     return FFmpegReader(path, f, w, h, rate, start=start, duration=duration)
+
+
+def audio_params(path):  # pragma: no cover - needs ffprobe
+    """(sample_rate, channel_layout) of the first audio stream, or None."""
+    try:
+        out = subprocess.run(["ffprobe", "-loglevel", "error", "-select_streams", "a", "-show_streams", "-of",
+                              "json", path], check=True, capture_output=True).stdout
+    except (OSError, subprocess.CalledProcessError):
+        return None
+    st = json.loads(out).get("streams", [])
+    if not st:
+        return None
+    return int(st[0]["sample_rate"]), st[0].get("channel_layout") or "stereo"
 
 
 def probe(path):
