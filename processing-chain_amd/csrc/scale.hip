@@ -26,7 +26,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
-#include <vector>
 #include <type_traits>
 
 #include "filters.hpp"
@@ -530,9 +529,7 @@ void row_chunks(HostPlane &hp, int sh, int dh, int cho, int seg_h, int *maxnew, 
         for (int y = ci * cho; y < std::min(dh, (ci + 1) * cho); ++y) top = std::max(top, hp.vbase[y] + 2 * hp.vtp);
         wr = std::max(wr, top - b);
     }
-    // the strip kernel's column walkers may start a fresh window at any chunk
-    // (the start of their unit range, or a frame boundary): a whole chunk span
-    mn = std::max(mn, span);
+    (void)span;
     *maxnew = std::max(mn, 1);
     *ring = (wr + 1) & ~1;
 }
@@ -870,8 +867,7 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
     const bool tw256 = P->job[0].tw == kTileW && P->job[1].tw == kTileW && P->job[2].tw == kTileW;
     KernelFn k;
     size_t lds = P->lds_bytes;
-    const bool strip = P->fast_hw && a.vec_src;
-    if (strip) {
+    if (P->fast_hw && a.vec_src) {
         for (int p = 0; p < 3; ++p) a.pl[p] = P->fjob[p];
         lds = P->fast_lds;
         const int vtm = strip_vtm_bucket(std::max(P->fjob[0].vtp, P->fjob[1].vtp));
@@ -882,50 +878,6 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
         k = out_depth == 8 ? pick_ht<uint16_t, 8>(P->ht, tw256) : pick_ht<uint16_t, 10>(P->ht, tw256);
     }
     if (!k) PP_FAIL(PP_ERR_UNSUPPORTED, "no kernel for %d taps", P->ht);
-    if (strip) {
-        // persistent column walkers: as many workgroups as are resident at
-        // once, split over the strip columns of the planes in proportion to
-        // their work (strip width x output rows x frames), each walking a
-        // contiguous range of (frame, chunk) units -- no tail, no per-segment
-        // start-up, no re-staged segment halo
-        // resident workgroups per CU: the occupancy API reports one too many at
-        // 81-112 SGPRs (MI355X_MICROARCH.md, residency), which would leave a
-        // second, tail-only round of workgroups; bound it by LDS and by the
-        // SGPR rule floor(800 / (ceil(sgpr/16)*16 + 16))
-        int per_cu = 0;
-        PP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, lds));
-        hipFuncAttributes fa{};
-        PP_HIP(hipFuncGetAttributes(&fa, (const void *)k));
-        per_cu = std::min<int>(per_cu, (int)(160 * 1024 / std::max<size_t>(lds, 1)));
-        if (const char *e = std::getenv("PIXPATH_SCALE_PER_CU")) per_cu = atoi(e);  // measurement only
-        const int G = std::max(1, per_cu) * std::max(1, P->ctx->cus);
-        struct Col { int ps; double work; int64_t units; };
-        std::vector<Col> cols;
-        double total = 0;
-        for (int p = 0; p < 3; ++p) {
-            const PlaneJob &J = P->fjob[p];
-            const int64_t units = (int64_t)nframes * ((J.dh + J.cho - 1) / J.cho);
-            for (int tx = 0; tx < J.tiles_x; ++tx) {
-                const double wk = (double)std::min(kTileW, J.dw - tx * kTileW) * J.dh * nframes;
-                cols.push_back({(p << 16) | tx, wk, units});
-                total += wk;
-            }
-        }
-        if ((int)cols.size() > kMaxCols) PP_FAIL(PP_ERR_UNSUPPORTED, "%d strip columns > %d", (int)cols.size(), kMaxCols);
-        a.nframes = nframes;
-        a.ncols = (int)cols.size();
-        int g = 0;
-        for (int c = 0; c < a.ncols; ++c) {
-            a.col_first[c] = g;
-            a.col_ps[c] = cols[c].ps;
-            const int64_t want = std::llround(G * cols[c].work / total);
-            g += (int)std::max<int64_t>(1, std::min<int64_t>(want, cols[c].units));
-        }
-        a.col_first[a.ncols] = g;
-        hipLaunchKernelGGL(k, dim3(g), dim3(kThreads), lds, st, a);
-        PP_HIP(hipGetLastError());
-        return PP_OK;
-    }
     const int tiles = P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y;
     a.tiles = tiles;
     const int fmax = std::max(1, (1 << 30) / tiles);  // 1-D grid size limit

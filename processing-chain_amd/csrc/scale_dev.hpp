@@ -18,7 +18,6 @@ constexpr int kTileW = 256;      // widest output tile (columns); narrower for l
 constexpr int kThreads = 256;    // 4 waves
 constexpr int kLdsBudget = 40 * 1024;
 constexpr int kChoMax = 32;     // output rows per chunk (upper bound)
-constexpr int kMaxCols = 96;      // strip columns over all planes (8K luma: 32 strips)
 constexpr int kSegRows = 540;   // output rows per segment (target; profiles/r2: 540 beats 256 by ~1.5 %)
 
 static __constant__ uint8_t c_dither[8][8] = {
@@ -59,14 +58,6 @@ struct ScaleArgs {
     int vec_src;  // all source rows 16-B aligned
     int vec_dst;  // all destination rows 8-B aligned (4 outputs per lane)
     int debug;    // ablation (measurement only, PIXPATH_SCALE_DEBUG): 1 no V stores, 2 no staging loads, 4 no H pass
-    // strip_kernel (persistent column walkers): workgroups col_first[c] ..
-    // col_first[c+1]-1 walk column c = (plane col_ps[c] >> 16, strip col_ps[c]
-    // & 0xffff) over units (frame, chunk) 0 .. nframes*chunks-1 in equal
-    // contiguous ranges
-    int nframes;
-    int ncols;
-    int col_first[kMaxCols + 1];
-    int col_ps[kMaxCols];
 };
 
 // Register prefetch of up to kPF 16-byte source chunks per lane (software

@@ -41,23 +41,21 @@ struct StripPrefetch {
 // else 4 (128 VGPRs) or 3 (168 VGPRs, the widest H windows).  tools/check_spills.sh checks every instance.
 template <int SB, int OUTB, int HW, int VTM>
 constexpr int strip_min_waves() {
-    return HW >= 12 ? 3 : (VTM <= 5 && HW <= (OUTB == 10 ? (SB == 2 ? 6 : 5) : 3)) ? 6 : 4;
+    return HW >= 12 ? 3 : (VTM <= 5 && HW <= (OUTB == 10 && SB == 2 ? 6 : 4)) ? 6 : 4;
 }
 
 template <typename ST, int OUTB, int HW, int VTM>
 __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
     extern __shared__ __align__(16) uint16_t lds[];
-    // ---- this workgroup's column and (frame, chunk) range ----------------------
-    const int w = blockIdx.x;
-    int c = 0;
-    while (c + 1 < a.ncols && w >= a.col_first[c + 1]) ++c;  // uniform scan of a short table
-    const int p = a.col_ps[c] >> 16, tx = a.col_ps[c] & 0xffff;
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int frame = L / a.tiles;
+    int t = L - frame * a.tiles;
+    int p = 0;
+    if (a.nplanes > 1 && t >= a.pl[1].tile_base) p = 1;
+    if (a.nplanes > 2 && t >= a.pl[2].tile_base) p = 2;
     const PlaneJob &J = a.pl[p];
-    const int cho = J.cho;
-    const int nch = (J.dh + cho - 1) / cho;
-    const int64_t units = (int64_t)a.nframes * nch;
-    const int gc = a.col_first[c + 1] - a.col_first[c], jw = w - a.col_first[c];
-    const int u_begin = (int)(units * jw / gc), u_end = (int)(units * (jw + 1) / gc);
+    t -= J.tile_base;
+    const int seg = t / J.tiles_x, tx = t - seg * J.tiles_x;
     const int x0 = tx * kTileW, nx = min(kTileW, J.dw - x0);
     const int c0 = as_kconst<int32_t>(J.tile_c0)[tx], cn = as_kconst<int32_t>(J.tile_cn)[tx];
     // chunk tables through the scalar cache: no vector-memory wait at chunk starts
@@ -69,6 +67,8 @@ __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, H
     const int cx = lane * 4;
     uint16_t *src_t = lds;                                                  // [maxnew][S]
     uint32_t *win = reinterpret_cast<uint32_t *>(lds + J.maxnew * S);       // [ring/2][256] row pairs
+    const ST *sbase = reinterpret_cast<const ST *>(a.src[p] + frame * a.sfs[p]);
+    uint8_t *dbase = a.dst[p] + frame * a.dfs[p];
 
     // ---- horizontal taps of this lane's 4 columns over its HW-dword window ----
     constexpr int hshift = sizeof(ST) == 1 ? 7 : 9;
@@ -99,16 +99,14 @@ __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, H
     const int64_t sls = a.sls[p];
     const int sw = J.sw;
     const int64_t last_row = std::min<int64_t>(sls, ((int64_t)sw * sizeof(ST) + 15) & ~int64_t(15));
-    const int plane_bytes = (int)((int64_t)(J.sh - 1) * sls + last_row);
-    // one buffer resource per frame plane: loads past it read 0
-    auto frame_rsrc = [&](int fr) { return uniform_rsrc(a.src[p] + (int64_t)fr * a.sfs[p], plane_bytes); };
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(sbase, (int)((int64_t)(J.sh - 1) * sls + last_row));
     const int cbyte = c0 * (int)sizeof(ST);
     const int s_rstep = kThreads / cpr;
     const int s_r0 = tid / cpr, s_ch = tid - s_r0 * cpr;
     const bool s_on = s_r0 < s_rstep;
     const int s_lds = s_r0 * S + s_ch * CH;
     const int s_goff = s_r0 * (int)sls + cbyte + s_ch * 16;
-    auto prefetch = [&](StripPrefetch &pf, __amdgpu_buffer_rsrc_t rs, int from, int hi_) {
+    auto prefetch = [&](StripPrefetch &pf, int from, int hi_) {
         const int nrow = hi_ - from;
 #pragma unroll
         for (int k = 0; k < kStripPF; ++k) {
@@ -116,7 +114,7 @@ __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, H
             pf.v[k] = bload16(rs, (s_on && r < nrow) ? s_goff + (from + k * s_rstep) * (int)sls : kOobOff);
         }
     };
-    auto commit = [&](const StripPrefetch &pf, __amdgpu_buffer_rsrc_t rs, int from, int hi_) {
+    auto commit = [&](const StripPrefetch &pf, int from, int hi_) {
         const int nrow = hi_ - from;
         if (!s_on) return;
 #pragma unroll
@@ -147,47 +145,37 @@ __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, H
         }
     };
 
-    // ---- the walk: units (frame, chunk) u_begin .. u_end-1 of this column ----
-    // Within a frame consecutive chunks share window rows (kept pairs); a new
-    // frame (or the range start) starts a fresh window.  The first unit's rows
-    // are staged before the loop; every later unit's rows are loaded right
-    // after the chunk-start barrier of the unit before -- across a frame
-    // boundary too, so a workgroup streams frame after frame with no exposed
-    // start-up -- and written to LDS right after its window barrier (src_t is
-    // free then).  Between those two points the wave issues no vector-memory
-    // op, so the wait for the loads never covers its own V-pass stores (vmcnt
-    // is in-order over loads and stores).
-    if (u_begin >= u_end) return;
-    int fr = u_begin / nch, ci = u_begin - fr * nch;
-    __amdgpu_buffer_rsrc_t rs = frame_rsrc(fr);
-    int next_src = chunk_lo[ci];
+    const int y_begin = seg * J.seg_h, y_end = min(J.dh, y_begin + J.seg_h);
+    const int cho = J.cho;
+    int next_src = chunk_lo[y_begin / cho];
     int base = next_src & ~1;
     StripPrefetch pf;
-    prefetch(pf, rs, next_src, chunk_hi[ci]);
-    commit(pf, rs, next_src, chunk_hi[ci]);
+    // the first chunk's rows are staged before the loop; every later chunk's
+    // rows are loaded right after the chunk-start barrier of the chunk before
+    // and written to LDS right after its window barrier (src_t is free then).
+    // Between those two points the wave issues no vector-memory op, so the
+    // wait for the loads never covers this wave's V-pass stores (vmcnt is
+    // in-order over loads and stores).
+    prefetch(pf, next_src, chunk_hi[y_begin / cho]);
+    commit(pf, next_src, chunk_hi[y_begin / cho]);
     const bool lane_any = cx < nx, lane_full = cx + 4 <= nx;
     const int xo = x0 + cx;
     const int64_t dls = a.dls[p];
     const int vtp = J.vtp;
     const kconst int32_t *vrow = as_kconst<int32_t>(J.vrow16);
-    for (int u = u_begin; u < u_end; ++u) {
-        const int y0 = ci * cho;
+    for (int y0 = y_begin; y0 < y_end; y0 += cho) {
+        const int ci = y0 / cho;
         const int lo = chunk_lo[ci], hi = chunk_hi[ci];
         if (next_src < lo) next_src = lo;
         const int nnew = hi - next_src;
         const int nbase = lo & ~1;
         const int keep = next_src > nbase ? (next_src - nbase + 1) >> 1 : 0;
         const int shift = (nbase - base) >> 1;
-        uint8_t *dbase = a.dst[p] + (int64_t)fr * a.dfs[p];
         if (!(a.debug & 8)) __syncthreads();  // staged rows visible; every wave has left the previous V pass
-        // the next unit: the next chunk of this frame, or chunk 0 of the next frame
-        const bool more = u + 1 < u_end;
-        const bool wrap = ci + 1 == nch;
-        const int nci = wrap ? 0 : ci + 1;
-        const __amdgpu_buffer_rsrc_t nrs = wrap ? frame_rsrc(fr + 1) : rs;
         const int after = nnew > 0 ? hi : next_src;
-        const int nfrom = more ? (wrap ? chunk_lo[0] : max(after, chunk_lo[nci])) : 0, nhi = more ? chunk_hi[nci] : 0;
-        if (more && !(a.debug & 2)) prefetch(pf, nrs, nfrom, nhi);
+        const bool more = y0 + cho < y_end;
+        const int nfrom = more ? max(after, chunk_lo[ci + 1]) : 0, nhi = more ? chunk_hi[ci + 1] : 0;
+        if (more && !(a.debug & 2)) prefetch(pf, nfrom, nhi);
         // kept row pairs move down to the window start, each column by its own
         // lane in increasing order (no lane reads a slot already overwritten)
         if (shift > 0) {
@@ -229,9 +217,9 @@ __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, H
             next_src = hi;
         }
         if (!(a.debug & 8)) __syncthreads();  // window complete; src_t is free
-        if (more && nhi > nfrom && !(a.debug & 2)) commit(pf, nrs, nfrom, nhi);
+        if (more && nhi > nfrom && !(a.debug & 2)) commit(pf, nfrom, nhi);
         // ---- vertical pass: one output row per wave --------------------------
-        const int ny = min(cho, J.dh - y0);
+        const int ny = min(cho, y_end - y0);
         // VT (= vtp) tap pairs, compile-time per instance: every window read of
         // a row is in flight before the first v_dot2 waits on one
         auto vpass = [&](auto vt_c) {
@@ -323,13 +311,6 @@ __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, H
         case 7: if constexpr (VTM >= 7) vpass(std::integral_constant<int, 7>{}); break;
         default: if constexpr (VTM >= 8) vpass(std::integral_constant<int, 8>{}); break;
         }
-        if (wrap) {  // the next frame starts a fresh window
-            ++fr;
-            rs = nrs;
-            next_src = chunk_lo[0];
-            base = next_src & ~1;
-        }
-        ci = nci;
     }
 }
 
