@@ -7,8 +7,9 @@
 //   SI_n = std over rows 1..H-2, cols 1..W-2 of sqrt(Gx^2 + Gy^2)  (Sobel 3x3)
 //   TI_n = std over the full frame of Y_n - Y_{n-1}                (n >= 1)
 //
-// Layout: a workgroup (256 lanes, 4 waves) owns a 2048-px x 16-row band of the frame
-// and walks a contiguous chunk of frames.  Each lane holds 8 adjacent pixels
+// Layout: a workgroup (256 lanes, 4 waves) owns a 1984-px x 16-row band of the
+// frame (4 x 496 px; lanes 0 and 63 of a wave are halo lanes) and walks a
+// contiguous chunk of frames.  Each lane holds 8 adjacent pixels
 // of a row (one 16-B or 8-B load), gets its left/right neighbours by lane
 // shuffles (global loads only at wave edges), and slides a 3-row window down
 // the band, so every pixel of the band is read from HBM once per frame; the
@@ -24,8 +25,14 @@
 // sum(d^2) exact in 64-bit integers.  Per (frame, band) partials are written
 // without atomics and reduced in a fixed order by siti_finalize, so results
 // are bit-reproducible.
+// Bound: VALU, not HBM -- the interior frame loop is ~1740 VALU instructions
+// per wave and frame for 8 x 16 pixels a lane (Sobel in packed 16-bit math,
+// one v_sqrt_f32 per pixel, TI by v_dot2), ~73 % VALU-busy at 0.68 ms on
+// config 2 (profiles/r2/siti_experiments.md).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 
 #include "common.hpp"
 #include "device.hpp"
@@ -57,12 +64,6 @@ __device__ inline void chan_merge(int64_t &n, double &mean, double &m2, int64_t 
     mean += delta * fb;
     m2 += m2b + delta * delta * static_cast<double>(n) * fb;
     n = nn;
-}
-
-__device__ inline uint64_t wave_sum_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
 }
 
 // One row of a lane's 8 pixels in load format: 4 dwords (u16) or 2 (u8).
@@ -129,16 +130,92 @@ __device__ inline void to_pairs(const Row<T> &r, uint32_t w[4]) {
     }
 }
 
+// Wave-wide sums without LDS round trips: quad permutes, the row mirrors,
+// then gfx950's 16- and 32-lane swaps.  Every step adds the same pair of
+// values on both lanes of the pair (IEEE addition commutes exactly), so all
+// lanes end with identical bits and the order is fixed: reproducible.
+template <int CTRL>
+__device__ inline uint32_t dpp32(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ inline double dpp64(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint64_t r = (uint64_t)dpp32<CTRL>((uint32_t)b) | ((uint64_t)dpp32<CTRL>((uint32_t)(b >> 32)) << 32);
+    return __builtin_bit_cast(double, r);
+}
+// the two values a lane's row pair (16-lane rows) / wave half pair hold
+__device__ inline void swap16(uint32_t v, uint32_t &a, uint32_t &b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    a = r[0]; b = r[1];
+}
+__device__ inline void swap32(uint32_t v, uint32_t &a, uint32_t &b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    a = r[0]; b = r[1];
+}
+template <typename V>
+__device__ inline V row_sum(V v) {  // sum over each 16-lane row
+    if constexpr (sizeof(V) == 8) {
+        v += dpp64<0xB1>(v);   // quad_perm [1,0,3,2]
+        v += dpp64<0x4E>(v);   // quad_perm [2,3,0,1]
+        v += dpp64<0x141>(v);  // row_half_mirror
+        v += dpp64<0x140>(v);  // row_mirror
+    } else {
+        v += (V)dpp32<0xB1>((uint32_t)v);
+        v += (V)dpp32<0x4E>((uint32_t)v);
+        v += (V)dpp32<0x141>((uint32_t)v);
+        v += (V)dpp32<0x140>((uint32_t)v);
+    }
+    return v;
+}
+__device__ inline double wave_sum_f64(double v) {
+    v = row_sum(v);
+    uint64_t b = __builtin_bit_cast(uint64_t, v);
+    uint32_t l0, l1, h0, h1;
+    swap16((uint32_t)b, l0, l1);
+    swap16((uint32_t)(b >> 32), h0, h1);
+    v = __builtin_bit_cast(double, (uint64_t)l0 | ((uint64_t)h0 << 32)) +
+        __builtin_bit_cast(double, (uint64_t)l1 | ((uint64_t)h1 << 32));
+    b = __builtin_bit_cast(uint64_t, v);
+    swap32((uint32_t)b, l0, l1);
+    swap32((uint32_t)(b >> 32), h0, h1);
+    return __builtin_bit_cast(double, (uint64_t)l0 | ((uint64_t)h0 << 32)) +
+           __builtin_bit_cast(double, (uint64_t)l1 | ((uint64_t)h1 << 32));
+}
+__device__ inline int wave_sum_i32(int v) {
+    v = row_sum(v);
+    uint32_t a, b;
+    swap16((uint32_t)v, a, b);
+    swap32(a + b, a, b);
+    return (int)(a + b);
+}
+// sum of u32 values whose 32-lane sums fit in 32 bits; the last step in 64
+__device__ inline uint64_t wave_sum_u32_wide(uint32_t v) {
+    v = row_sum(v);
+    uint32_t a, b;
+    swap16(v, a, b);
+    swap32(a + b, a, b);
+    return (uint64_t)a + (uint64_t)b;
+}
+
 // Window of a workgroup's band: rows y0-1 .. y0+kBand of one frame, held as
 // raw load registers.  Row ri's registers are reloaded with the NEXT frame's
 // row ri right after frame f consumes them, so a whole frame of loads is in
 // flight while the current one is computed, with no extra registers and no
 // branches around the loads.  The previous frame's band (TI) stays in
 // registers too, so every pixel is read from HBM once (plus the two halo rows).
-template <typename T>
-__device__ __forceinline__ void siti_range(const uint8_t *frames, int64_t ls, int64_t fs, int nframes,
-                                          const uint8_t *prev, int W, int H, int tiles_x, int tile, int f0, int f1,
-                                          SitiPartial *part) {
+//
+// INTERIOR (every band but the first and the last): all 18 window rows lie in
+// the frame and all 16 Sobel centres are valid, so the unrolled row loop has
+// no per-row conditions at all (they cost SGPRs, spilled to VGPR lanes, and a
+// branch per row).  Lanes outside the frame and the halo lanes carry no TI
+// samples: their TI sums are dropped once per frame instead of masking every
+// pixel; only a lane straddling a ragged right edge (RAGGED: W % 8 != 0) masks
+// its pixels.  The next frame's rows are read through a descriptor of 0 bytes
+// after the range's last frame (no traffic, no per-row liveness test).
+template <typename T, bool INTERIOR, bool RAGGED>
+__device__ __forceinline__ void siti_range(const uint8_t *frames, int64_t ls, int64_t fs, const uint8_t *prev, int W,
+                                          int H, int tiles_x, int tile, int f0, int f1, SitiPartial *part) {
     constexpr int NR = kBand + 2;
     const int bands = (H + kBand - 1) / kBand;
     const int tx = tile % tiles_x, band = tile / tiles_x;
@@ -150,47 +227,45 @@ __device__ __forceinline__ void siti_range(const uint8_t *frames, int64_t ls, in
     const int y0 = band * kBand, y1 = min(H, y0 + kBand);
     // lane-relative valid Sobel columns [lo, hi] (empty for halo lanes)
     const int sobel_lo = halo ? kLanePx : 1 - x, sobel_hi = halo ? -1 : W - 2 - x;
+    // TI: lanes whose 8 pixels are all frame pixels the wave accounts for; the
+    // straddling lane of a ragged edge masks per pixel
+    const bool ti_lane = !halo && x >= 0 && x < W;
 
     // a row load straddling num_records reads 0 as a whole: the last row counts
     // up to its load-granule-rounded width, which lies inside the (aligned) pitch
     constexpr int G = kLanePx * sizeof(T);
     const int frame_bytes = (int)((int64_t)(H - 1) * ls + min(ls, ((int64_t)W * sizeof(T) + G - 1) / G * G));
-    const int xb = x * (int)sizeof(T);
     const bool x_in = x >= 0 && x < W;  // lane 0 of the first wave sits left of the frame
-    auto rsrc = [&](const uint8_t *base) { return uniform_rsrc(base, frame_bytes); };
-    auto row_off = [&](int r, bool live) { return (live && x_in && r >= 0 && r < H) ? r * (int)ls + xb : kOob; };
+    // row r of a frame at lane offset voff + r * ls (unsigned: row -1 and rows
+    // >= H fall outside num_records and read 0; so does every row of a lane
+    // outside the frame, which starts at kOob)
+    const uint32_t voff = x_in ? (uint32_t)(x * (int)sizeof(T)) : (uint32_t)kOob;
+    const uint32_t uls = (uint32_t)ls;
+    auto row_off = [&](int r) { return voff + (uint32_t)r * uls; };
 
     Row<T> raw[NR], pv[kBand];
     // previous frame's band
     const uint8_t *pfirst = f0 > 0 ? frames + (f0 - 1) * fs : prev;
-    const bool have_pfirst = pfirst != nullptr && f0 < f1;
     {
-        const auto prs = rsrc(have_pfirst ? pfirst : frames);
+        const auto prs = uniform_rsrc(pfirst ? pfirst : frames, pfirst ? frame_bytes : 0);
 #pragma unroll
-        for (int i = 0; i < kBand; ++i) {
-            issue_row<T>(pv[i], prs, row_off(y0 + i, have_pfirst && y0 + i < y1));
-        }
+        for (int i = 0; i < kBand; ++i) issue_row<T>(pv[i], prs, row_off(y0 + i));
     }
     // first frame's window
     {
-        const uint8_t *fb = frames + (int64_t)f0 * fs;
-        const bool live = f0 < f1;
-        const auto crs = rsrc(live ? fb : frames);
+        const auto crs = uniform_rsrc(frames + (int64_t)f0 * fs, frame_bytes);
 #pragma unroll
-        for (int ri = 0; ri < NR; ++ri) {
-            const int r = y0 - 1 + ri;
-            issue_row<T>(raw[ri], crs, row_off(r, live));
-        }
+        for (int ri = 0; ri < NR; ++ri) issue_row<T>(raw[ri], crs, row_off(y0 - 1 + ri));
     }
 
     // per-lane constants of the packed formulation
-    uint32_t tmask[4];  // TI: 0xffff per pixel this lane accounts for
+    uint32_t tmask[4];  // TI: 0xffff per pixel this lane accounts for (RAGGED only)
     v2f32 vm[4];        // Sobel: 1.0 per valid Sobel column, else 0
     int rc = 0;         // valid Sobel columns of this lane
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int e0 = 2 * k, e1 = 2 * k + 1;
-        const bool t0 = !halo && x + e0 >= 0 && x + e0 < W, t1 = !halo && x + e1 >= 0 && x + e1 < W;
+        const bool t0 = x + e0 < W, t1 = x + e1 < W;
         tmask[k] = (t0 ? 0xffffu : 0u) | (t1 ? 0xffff0000u : 0u);
         const bool s0 = e0 >= sobel_lo && e0 <= sobel_hi, s1 = e1 >= sobel_lo && e1 <= sobel_hi;
         vm[k] = v2f32{s0 ? 1.f : 0.f, s1 ? 1.f : 0.f};
@@ -201,15 +276,56 @@ __device__ __forceinline__ void siti_range(const uint8_t *frames, int64_t ls, in
     const int sobel_rows = max(0, min(y1 - 1, H - 2) - max(y0, 1) + 1);
     const bool row2_valid = y0 >= 1 && y0 < y1 && y0 <= H - 2;
     const double n_lane = static_cast<double>(rc) * sobel_rows;
+    // the wave's Sobel sample count: the same for every frame
+    const double cnt_w = wave_sum_f64(n_lane);
     // the lane's first valid Sobel column supplies the frame's shift K
     const int kpick = halo ? 0 : max(0, min(kLanePx - 1, sobel_lo));
     const uint32_t ones = 0x00010001u;
 
+    // Frame f's lane sums are reduced across the wave in the middle of frame
+    // f+1's rows (the range's last frame after the loop), so the reduction's
+    // dependent chains overlap independent row work.  fp64 in a fixed order:
+    // sum (n K + S1) -> mean_w, then sum (x - mean_w)^2 = sum (S2 + 2 dK S1 +
+    // n dK^2), dK = K - mean_w; TI moments as integers (|sum d| < 2^31 over a
+    // wave; sum d^2 of 32 lanes < 2^32, the last step in 64 bits).  The store
+    // is a buffer store whose offset is out of range on every lane but lane 0
+    // of a pending frame: no branch, the frame loop stays one basic block.
+    auto reduce_store = [&](int fq, bool live, float Kq, double l1, double l2, int q1, uint32_t q2, bool hp) {
+        const double sum = wave_sum_f64(n_lane * static_cast<double>(Kq) + l1);
+        const double mean_w = cnt_w > 0.0 ? sum / cnt_w : 0.0;
+        const double dk = static_cast<double>(Kq) - mean_w;
+        const double m2 = wave_sum_f64(l2 + 2.0 * dk * l1 + n_lane * dk * dk);
+        const int d1 = wave_sum_i32(ti_lane ? q1 : 0);
+        const uint64_t d2w = wave_sum_u32_wide(ti_lane ? q2 : 0u);
+        const int64_t idx = ((int64_t)max(fq, 0) * tiles_x * bands + tile) * 4 + wave;
+        const auto prs = uniform_rsrc(part + idx, (int)sizeof(SitiPartial));
+        const uint32_t o = (live && lane == 0) ? 0u : static_cast<uint32_t>(kOob);
+        const uint64_t n64 = static_cast<uint64_t>(static_cast<int64_t>(cnt_w));
+        const uint64_t d164 = hp ? static_cast<uint64_t>(static_cast<int64_t>(d1)) : 0u;
+        const uint64_t d264 = hp ? d2w : 0u;
+        const uint64_t mb = __builtin_bit_cast(uint64_t, mean_w), qb = __builtin_bit_cast(uint64_t, m2);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        auto pack = [](uint64_t a, uint64_t b) {
+            return u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+        };
+        __builtin_amdgcn_raw_buffer_store_b128(pack(mb, qb), prs, o, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(pack(n64, d164), prs, o + 16, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(pack(d264, 0), prs, o + 32, 0, 0);
+    };
+    bool pend = false, p_hp = false;
+    float p_K = 0.f;
+    double p_l1 = 0.0, p_l2 = 0.0;
+    int p_d1 = 0;
+    uint32_t p_d2 = 0;
+
     for (int f = f0; f < f1; ++f) {
         const bool has_prev = f > 0 || prev != nullptr;
         const bool nlive = f + 1 < f1;
-        const uint8_t *nb = frames + (int64_t)(nlive ? f + 1 : f) * fs;
-        const auto nrs = rsrc(nb);
+        const auto nrs = uniform_rsrc(frames + (int64_t)(nlive ? f + 1 : f) * fs, nlive ? frame_bytes : 0);
+        // the row offsets are frame-invariant: recompute them per frame (one
+        // SALU op a row) instead of letting 18 hoisted values spill
+        uint32_t fls = uls;
+        asm volatile("" : "+s"(fls));
         // shifted moments of |G|: x = |G| - K over the lane's valid columns,
         // S1 = sum x, S2 = sum x^2 (K = one of the lane's own samples, so a
         // constant-magnitude frame gives x = 0 exactly and SI = 0 exactly)
@@ -234,18 +350,20 @@ __device__ __forceinline__ void siti_range(const uint8_t *frames, int64_t ls, in
                 // (v[2k-1], v[2k]) and (v[2k+1], v[2k+2]) as u16 pairs
                 const uint32_t lp = __builtin_amdgcn_alignbit(w[k], k ? w[k - 1] : wl, 16);
                 const uint32_t rp = __builtin_amdgcn_alignbit(k < 3 ? w[k + 1] : wr, w[k], 16);
-                h1[k] = pk_sub(rp, lp);                    // right - left         (|.| <= 1023)
+                h1[k] = pk_sub(rp, lp);                      // right - left         (|.| <= 1023)
                 h2[k] = pk_add(pk_2a_plus_b(w[k], lp), rp);  // left + 2 v + right (<= 4092)
             }
             // TI on the band rows against the previous frame's band
             const int bi = ri - 1;
             if (ri >= 1 && ri <= kBand) {
-                if (has_prev && r < y1) {
+                if (INTERIOR || r < y1) {
                     uint32_t q[4];
                     to_pairs<T>(pv[bi], q);
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
-                        const v2i16 d = __builtin_bit_cast(v2i16, pk_sub(w[k], q[k]) & tmask[k]);
+                        uint32_t dd = pk_sub(w[k], q[k]);
+                        if constexpr (RAGGED) dd &= tmask[k];
+                        const v2i16 d = __builtin_bit_cast(v2i16, dd);
                         d1s = __builtin_amdgcn_sdot2(d, __builtin_bit_cast(v2i16, ones), d1s, false);
                         d2s = static_cast<uint32_t>(__builtin_amdgcn_sdot2(d, d, static_cast<int>(d2s), false));
                     }
@@ -254,7 +372,7 @@ __device__ __forceinline__ void siti_range(const uint8_t *frames, int64_t ls, in
             }
             // Sobel centred on row c = r - 1 (rows c-1, c, c+1 are in the window)
             const int c = r - 1;
-            if (ri >= 2 && c < y1 && c >= 1 && c <= H - 2) {
+            if (ri >= 2 && (INTERIOR || (c < y1 && c >= 1 && c <= H - 2))) {
                 v2f32 mag[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -266,7 +384,8 @@ __device__ __forceinline__ void siti_range(const uint8_t *frames, int64_t ls, in
                     const int g0 = sq_norm(p0), g1 = sq_norm(p1);
                     mag[k] = v2f32{__fsqrt_rn(static_cast<float>(g0)), __fsqrt_rn(static_cast<float>(g1))};
                 }
-                if (ri == 2 || (ri == 3 && !row2_valid)) {  // first valid Sobel row of the band
+                // first valid Sobel row of the band
+                if (INTERIOR ? ri == 2 : (ri == 2 || (ri == 3 && !row2_valid))) {
                     float k = mag[0].x;
 #pragma unroll
                     for (int e = 1; e < kLanePx; ++e) k = kpick == e ? ((e & 1) ? mag[e >> 1].y : mag[e >> 1].x) : k;
@@ -288,34 +407,18 @@ __device__ __forceinline__ void siti_range(const uint8_t *frames, int64_t ls, in
                 h1b[k] = h1[k]; h2b[k] = h2[k];
             }
             // this row is consumed: start loading the next frame's row ri into it
-            issue_row<T>(raw[ri], nrs, row_off(r, nlive));
+            issue_row<T>(raw[ri], nrs, voff + (uint32_t)r * fls);
+            if (ri == 6) reduce_store(f - 1, pend, p_K, p_l1, p_l2, p_d1, p_d2, p_hp);
         }
-        // wave reduction in fp64, fixed butterfly order: N, sum (n K + S1) -> mean_w,
-        // then sum (x - mean_w)^2 = sum (S2 + 2 dK S1 + n dK^2), dK = K - mean_w;
-        // TI moments as integers
-        const double ls1 = static_cast<double>(s1.x) + static_cast<double>(s1.y);
-        const double ls2 = static_cast<double>(s2.x) + static_cast<double>(s2.y);
-        double cnt = n_lane, sum = n_lane * static_cast<double>(K) + ls1;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            cnt += __shfl_xor(cnt, o, 64);
-            sum += __shfl_xor(sum, o, 64);
-        }
-        const double mean_w = cnt > 0.0 ? sum / cnt : 0.0;
-        const double dk = static_cast<double>(K) - mean_w;
-        double m2 = ls2 + 2.0 * dk * ls1 + n_lane * dk * dk;
-        int64_t d1 = d1s;
-        uint64_t d2 = d2s;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            m2 += __shfl_xor(m2, o, 64);
-            d1 += __shfl_xor(d1, o, 64);
-            d2 += __shfl_xor(d2, o, 64);
-        }
-        if (lane == 0)
-            part[((int64_t)f * tiles_x * bands + tile) * 4 + wave] = {mean_w, m2, static_cast<int64_t>(cnt), d1,
-                                                                       d2, 0};
+        pend = true;
+        p_hp = has_prev;
+        p_K = K;
+        p_l1 = static_cast<double>(s1.x) + static_cast<double>(s1.y);
+        p_l2 = static_cast<double>(s2.x) + static_cast<double>(s2.y);
+        p_d1 = d1s;
+        p_d2 = d2s;
     }
+    if (pend) reduce_store(f1 - 1, true, p_K, p_l1, p_l2, p_d1, p_d2, p_hp);
 }
 
 // 1-D grid sized to the resident workgroup slots; workgroup i walks the
@@ -324,10 +427,10 @@ __device__ __forceinline__ void siti_range(const uint8_t *frames, int64_t ls, in
 // band count does not divide them) and at most one band switch per range.
 // XCD-aware: an XCD holds consecutive ranges, i.e. adjacent bands advancing
 // through the same frames together, so the halo rows they share hit its L2.
-template <typename T>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void siti_kernel(const uint8_t *frames, int64_t ls, int64_t fs, int nframes,
-                                                   const uint8_t *prev, int W, int H, int tiles_x, int ntiles,
-                                                   SitiPartial *part) {
+template <typename T, bool RAGGED>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void siti_kernel(
+    const uint8_t *frames, int64_t ls, int64_t fs, int nframes, const uint8_t *prev, int W, int H, int tiles_x,
+    int ntiles, SitiPartial *part) {
     const int64_t total = (int64_t)ntiles * nframes;
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     int64_t u = total * L / gridDim.x;
@@ -336,7 +439,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
         const int tile = (int)(u / nframes);
         const int f0 = (int)(u - (int64_t)tile * nframes);
         const int f1 = (int)min<int64_t>(nframes, f0 + (u1 - u));
-        siti_range<T>(frames, ls, fs, nframes, prev, W, H, tiles_x, tile, f0, f1, part);
+        const int y0 = tile / tiles_x * kBand;
+        if (y0 >= 1 && y0 + kBand + 1 <= H)
+            siti_range<T, true, RAGGED>(frames, ls, fs, prev, W, H, tiles_x, tile, f0, f1, part);
+        else
+            siti_range<T, false, RAGGED>(frames, ls, fs, prev, W, H, tiles_x, tile, f0, f1, part);
         u += f1 - f0;
     }
 }
@@ -393,14 +500,19 @@ extern "C" int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma
     hipStream_t st = static_cast<hipStream_t>(stream);
     PP_HIP(hipSetDevice(ctx->device));
     const int bytes = bitdepth > 8 ? 2 : 1;
-    const int tiles_x = (w + kSpan - 1) / kSpan, bands = (h + kBand - 1) / kBand;
+    const int tiles_x = (w + kSpan - 1) / kSpan;
+    const int bands = (h + kBand - 1) / kBand;
     const int ntiles = tiles_x * bands;
+    const bool ragged = (w % kLanePx) != 0;
+    using KFn = void (*)(const uint8_t *, int64_t, int64_t, int, const uint8_t *, int, int, int, int, SitiPartial *);
+    const KFn k = bytes == 2 ? (ragged ? siti_kernel<uint16_t, true> : siti_kernel<uint16_t, false>)
+                             : (ragged ? siti_kernel<uint8_t, true> : siti_kernel<uint8_t, false>);
+    const void *kfn = reinterpret_cast<const void *>(k);
     // one wave of resident workgroups (a partial second wave would idle most of
     // the chip), each walking an equal share of the (tile, frame) units
     int dev_cus = 0, per_cu = 0;
     PP_HIP(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    PP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, bytes == 2 ? (const void *)siti_kernel<uint16_t> : (const void *)siti_kernel<uint8_t>, 256, 0));
+    PP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, 0));
     const int64_t slots = std::max(1, dev_cus * std::max(1, per_cu));
     const int groups = (int)std::min<int64_t>(slots, (int64_t)ntiles * nframes);
     // The kernel reads each lane's 8 pixels as one 16-B (8-B) buffer load, so
@@ -416,8 +528,19 @@ extern "C" int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma
     if (!aligned) {
         ls = ((int64_t)w * bytes + 15) & ~int64_t(15);
         fs = ls * h;
+    }
+    // checked before any allocation, so a refused call leaks nothing
+    if ((int64_t)(h - 1) * ls + (int64_t)w * bytes >= (int64_t)kOob)
+        PP_FAIL(PP_ERR_UNSUPPORTED, "frame of %lld bytes exceeds the 2 GiB buffer range", (long long)(h * ls));
+    SitiPartial *part = nullptr;
+    PP_HIP(hipMallocAsync((void **)&part, sizeof(SitiPartial) * (size_t)ntiles * 4 * nframes, st));
+    if (!aligned) {
         const int nf = nframes + (prev ? 1 : 0);
-        PP_HIP(hipMallocAsync((void **)&scratch, (size_t)(fs * nf), st));
+        const hipError_t e = hipMallocAsync((void **)&scratch, (size_t)(fs * nf), st);
+        if (e != hipSuccess) {
+            (void)hipFreeAsync(part, st);
+            PP_FAIL(PP_ERR_HIP, "siti scratch (%lld bytes): %s", (long long)(fs * nf), hipGetErrorString(e));
+        }
         uint8_t *dst = scratch + (prev ? fs : 0);
         if (nframes == 1 || frame_stride == linesize * h) {
             PP_HIP(hipMemcpy2DAsync(dst, ls, luma, linesize, (size_t)w * bytes, (size_t)h * nframes,
@@ -432,11 +555,6 @@ extern "C" int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma
         src = dst;
         psrc = prev ? scratch : nullptr;
     }
-    if ((int64_t)(h - 1) * ls + (int64_t)w * bytes >= (int64_t)kOob)
-        PP_FAIL(PP_ERR_UNSUPPORTED, "frame of %lld bytes exceeds the 2 GiB buffer range", (long long)(h * ls));
-    SitiPartial *part = nullptr;
-    PP_HIP(hipMallocAsync((void **)&part, sizeof(SitiPartial) * (size_t)ntiles * 4 * nframes, st));
-    auto k = bytes == 2 ? siti_kernel<uint16_t> : siti_kernel<uint8_t>;
     hipLaunchKernelGGL(k, dim3(groups), dim3(256), 0, st, src, ls, fs, nframes, psrc, w, h, tiles_x, ntiles, part);
     hipLaunchKernelGGL(siti_finalize, dim3(nframes), dim3(256), 0, st, part, nframes, ntiles * 4, w, h,
                        prev != nullptr, si, ti);  // ntiles * 4 wave partials per frame

@@ -219,6 +219,9 @@ __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, H
         if (!(a.debug & 8)) __syncthreads();  // window complete; src_t is free
         if (more && nhi > nfrom && !(a.debug & 2)) commit(pf, nfrom, nhi);
         // ---- vertical pass: one output row per wave --------------------------
+        // raised priority while the wave issues its output rows: the other
+        // waves' H pass never starves the write stream (-2 %, profiles/r2)
+        __builtin_amdgcn_s_setprio(1);
         const int ny = min(cho, y_end - y0);
         // VT (= vtp) tap pairs, compile-time per instance: every window read of
         // a row is in flight before the first v_dot2 waits on one
@@ -311,6 +314,7 @@ __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, H
         case 7: if constexpr (VTM >= 7) vpass(std::integral_constant<int, 7>{}); break;
         default: if constexpr (VTM >= 8) vpass(std::integral_constant<int, 8>{}); break;
         }
+        __builtin_amdgcn_s_setprio(0);
     }
 }
 
