@@ -4,10 +4,14 @@
 //  pp_v210_pack       v210enc     lib/test_config.py:208-215 via lib/ffmpeg.py:1198
 //  pp_stall_compose   bufferer    p03_generateAvPvs.py:236-243 (spec PP-STALL-1)
 //
-// All are pure streaming kernels (HBM-bound, no reuse): one lane owns 16 bytes
-// of output, blockIdx.z walks the frames of the batch, so one launch covers a
-// whole batch.
+// All are pure streaming kernels (HBM-bound, no reuse).  Layout: one wave per
+// output row of one plane (1-D grid over frames x rows of all three planes,
+// XCD-remapped), each lane moving up to four 16-B chunks with every load in
+// flight before the first store -- full lanes on chroma rows too, and enough
+// bytes in flight per CU to cover HBM latency.  v210 packing goes through the
+// fused CPVS kernel (cpvs.hip) with a zero pad.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -15,142 +19,192 @@
 
 namespace pp {
 
+constexpr int kRowLanes = 64;  // one wave per row
+constexpr int kRowUnroll = 4;  // 16-B chunks a lane keeps in flight
+
+// Per-plane geometry of a row kernel launch.
+struct RowPlane {
+    const uint8_t *src;
+    int64_t sls, sfs;
+    uint8_t *dst;
+    int64_t dls, dfs;
+    int W, rows;       // output plane width (samples) and rows
+    int iw, ih;        // source plane size
+    int ox, oy;        // source offset on the output plane (pad); 0 for stall
+    int black;
+    int vec;           // source rows 16-B aligned and ox * EB % 16 == 0: vector loads
+    int dvec;          // destination rows 16-B aligned: vector stores
+};
+
+// 16-B chunk of output samples [x, x + N) of a row: the source row shifted by
+// ox, black outside [0, iw) (and for a null row).
+template <typename T>
+__device__ inline uint4 shifted_chunk(const T *srow, int x, int ox, int iw, int black, bool vec) {
+    constexpr int N = 16 / (int)sizeof(T);
+    const int sx = x - ox;
+    if (srow && vec && sx >= 0 && sx + N <= iw) return *reinterpret_cast<const uint4 *>(srow + sx);
+    T v[N];
+#pragma unroll
+    for (int e = 0; e < N; ++e) v[e] = (srow && sx + e >= 0 && sx + e < iw) ? srow[sx + e] : static_cast<T>(black);
+    uint4 r;
+    __builtin_memcpy(&r, v, 16);
+    return r;
+}
+
+template <typename T>
+__device__ inline void put_chunk(T *drow, int x, int W, bool dvec, const uint4 &v) {
+    constexpr int N = 16 / (int)sizeof(T);
+    if (dvec && x + N <= W) {
+        *reinterpret_cast<uint4 *>(drow + x) = v;
+    } else {
+        T e[N];
+        __builtin_memcpy(e, &v, 16);
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (x + i < W) drow[x + i] = e[i];
+    }
+}
+
+// unit -> (frame, plane, row) of a row-kernel grid over frames x (rows of planes 0, 1, 2)
+__device__ inline void row_unit(int unit, const RowPlane *pl, int &frame, int &p, int &y) {
+    const int rows = pl[0].rows + pl[1].rows + pl[2].rows;
+    frame = unit / rows;
+    y = unit - frame * rows;
+    p = 0;
+    if (y >= pl[0].rows) { y -= pl[0].rows; p = 1; }
+    if (p == 1 && y >= pl[1].rows) { y -= pl[1].rows; p = 2; }
+}
+
 // ---------------------------------------------------------------------------
 // vf_pad: out = black, except the (x, y)-shifted input.  EB = bytes per sample.
-template <int EB>
-__global__ __launch_bounds__(256) void pad_kernel(const uint8_t *src, int64_t sls, int64_t sfs, int iw, int ih,
-                                                  uint8_t *dst, int64_t dls, int64_t dfs, int W, int H, int ox,
-                                                  int oy, int black) {
-    using T = typename std::conditional<EB == 1, uint8_t, uint16_t>::type;
-    constexpr int N = 16 / EB;  // samples per lane
-    const int frame = blockIdx.z, y = blockIdx.y;
-    const T *srow = (y >= oy && y < oy + ih)
-                        ? reinterpret_cast<const T *>(src + frame * sfs + (int64_t)(y - oy) * sls)
-                        : nullptr;
-    T *drow = reinterpret_cast<T *>(dst + frame * dfs + (int64_t)y * dls);
-    for (int x = (blockIdx.x * 256 + threadIdx.x) * N; x < W; x += gridDim.x * 256 * N) {
-        T v[N];
-#pragma unroll
-        for (int e = 0; e < N; ++e) {
-            const int sx = x + e - ox;
-            v[e] = (srow && sx >= 0 && sx < iw) ? srow[sx] : static_cast<T>(black);
-        }
-        if (x + N <= W && ((reinterpret_cast<uintptr_t>(drow + x) & 15) == 0)) {
-            *reinterpret_cast<uint4 *>(drow + x) = *reinterpret_cast<const uint4 *>(v);
-        } else {
-#pragma unroll
-            for (int e = 0; e < N; ++e)
-                if (x + e < W) drow[x + e] = v[e];
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// v210: 6 pixels -> 4 LE32 words [U0 Y0 V0][Y1 U1 Y2][V1 Y3 U2][Y4 V2 Y5],
-// samples clipped to [4, 1019]; line = ceil(w/48)*48*8/3 bytes, zero padded.
-__device__ inline uint32_t v210c(uint32_t v) { return v < 4 ? 4 : (v > 1019 ? 1019 : v); }
-
-__global__ __launch_bounds__(256) void v210_kernel(const uint8_t *Yp, const uint8_t *Up, const uint8_t *Vp,
-                                                   int64_t yls, int64_t uls, int64_t vls, int64_t yfs, int64_t ufs,
-                                                   int64_t vfs, uint8_t *dst, int64_t dls, int64_t dfs, int w,
-                                                   int chunks) {
-    const int frame = blockIdx.z, row = blockIdx.y;
-    const uint16_t *y = reinterpret_cast<const uint16_t *>(Yp + frame * yfs + (int64_t)row * yls);
-    const uint16_t *u = reinterpret_cast<const uint16_t *>(Up + frame * ufs + (int64_t)row * uls);
-    const uint16_t *v = reinterpret_cast<const uint16_t *>(Vp + frame * vfs + (int64_t)row * vls);
-    uint4 *d = reinterpret_cast<uint4 *>(dst + frame * dfs + (int64_t)row * dls);
-    const int full = w / 6;
-    for (int q = blockIdx.x * 256 + threadIdx.x; q < chunks; q += gridDim.x * 256) {
-        uint4 o = {0, 0, 0, 0};
-        if (q < full) {
-            const int px = 6 * q, cx = 3 * q;
-            o.x = v210c(u[cx]) | (v210c(y[px]) << 10) | (v210c(v[cx]) << 20);
-            o.y = v210c(y[px + 1]) | (v210c(u[cx + 1]) << 10) | (v210c(y[px + 2]) << 20);
-            o.z = v210c(v[cx + 1]) | (v210c(y[px + 3]) << 10) | (v210c(u[cx + 2]) << 20);
-            o.w = v210c(y[px + 4]) | (v210c(v[cx + 2]) << 10) | (v210c(y[px + 5]) << 20);
-        } else if (q == full) {
-            // v210_enc_10 tail for w % 6 in {2..5}
-            const int r = w - 6 * full, px = 6 * full, cx = 3 * full;
-            if (r >= 2) {
-                o.x = v210c(u[cx]) | (v210c(y[px]) << 10) | (v210c(v[cx]) << 20);
-                uint32_t val = v210c(y[px + 1]);
-                if (r == 2) o.y = val;
-                if (r >= 4) {
-                    o.y = val | (v210c(u[cx + 1]) << 10) | (v210c(y[px + 2]) << 20);
-                    o.z = v210c(v[cx + 1]) | (v210c(y[px + 3]) << 10);
-                }
-            }
-        }
-        d[q] = o;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// PP-STALL-1 compositing.  One output frame per blockIdx.z; the spinner
-// region (sw x sh luma at (ox, oy)) is alpha-blended, everything else copied
-// (or black).  Spinner frame s: Y[sw*sh] Al[sw*sh] U V Ac[(sw>>hs)*(sh>>vs)] u16.
-struct StallArgs {
-    const uint8_t *src[3];
-    int64_t sls[3], sfs[3];
-    uint8_t *dst[3];
-    int64_t dls[3], dfs[3];
-    int32_t idx[2 * 256]; // per output frame of this launch: src index, spinner index
-    const uint16_t *spin; // spinner frames
-    int64_t spin_stride;  // elements per spinner frame
-    int w, h, hs, vs, depth, sw, sh, ox, oy;
+struct PadArgs {
+    RowPlane pl[3];
 };
 
 template <int EB>
-__global__ __launch_bounds__(256) void stall_kernel(const StallArgs a) {
+__global__ __launch_bounds__(kRowLanes) void pad_kernel(const PadArgs a) {
     using T = typename std::conditional<EB == 1, uint8_t, uint16_t>::type;
     constexpr int N = 16 / EB;
-    const int frame = blockIdx.z;
-    const int p = blockIdx.y >= a.h ? (blockIdx.y - a.h >= (a.h >> a.vs) ? 2 : 1) : 0;
-    const int y = p == 0 ? blockIdx.y : (blockIdx.y - a.h - (p == 2 ? (a.h >> a.vs) : 0));
-    const int W = p ? (a.w >> a.hs) : a.w;
+    int frame, p, y;
+    row_unit(xcd_remap(blockIdx.x, gridDim.x), a.pl, frame, p, y);
+    const RowPlane &g = a.pl[p];
+    const int iy = y - g.oy;
+    const T *srow = (iy >= 0 && iy < g.ih) ? reinterpret_cast<const T *>(g.src + frame * g.sfs + (int64_t)iy * g.sls)
+                                           : nullptr;
+    T *drow = reinterpret_cast<T *>(g.dst + frame * g.dfs + (int64_t)y * g.dls);
+    const int chunks = (g.W + N - 1) / N;
+    for (int q0 = threadIdx.x; q0 < chunks; q0 += kRowLanes * kRowUnroll) {
+        uint4 v[kRowUnroll];
+#pragma unroll
+        for (int u = 0; u < kRowUnroll; ++u) {
+            const int q = q0 + u * kRowLanes;
+            if (q < chunks) v[u] = shifted_chunk<T>(srow, q * N, g.ox, g.iw, g.black, g.vec);
+        }
+#pragma unroll
+        for (int u = 0; u < kRowUnroll; ++u) {
+            const int q = q0 + u * kRowLanes;
+            if (q < chunks) put_chunk<T>(drow, q * N, g.W, g.dvec, v[u]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// PP-STALL-1 compositing.  Output frame k of the launch shows source frame
+// idx[2k] (black if < 0) with spinner frame idx[2k+1] (none if < 0): the
+// spinner region (sw x sh luma at (ox, oy)) is alpha-blended, everything else
+// copied.  Spinner frame s: Y[sw*sh] Al[sw*sh] U V Ac[(sw>>hs)*(sh>>vs)] u16.
+struct StallArgs {
+    RowPlane pl[3];
+    int32_t idx[2 * 256];  // per output frame of this launch: src index, spinner index
+    const uint16_t *spin;  // spinner frames
+    int64_t spin_stride;   // elements per spinner frame
+    int hs, vs, sw, sh, ox, oy;
+    int nk, G;             // output frames in this launch, frames per tile
+};
+
+template <int EB>
+__global__ __launch_bounds__(kRowLanes) void stall_kernel(const StallArgs a) {
+    using T = typename std::conditional<EB == 1, uint8_t, uint16_t>::type;
+    constexpr int N = 16 / EB;
+    // units in tiles of G output frames: a tile walks the rows, each row of
+    // its G frames in turn, so a source row comes from the XCD's L2 for all
+    // but the first of them (G = 1: frame-major; G = all: row-major)
+    const int rows = a.pl[0].rows + a.pl[1].rows + a.pl[2].rows;
+    const int unit = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = unit / (rows * a.G), wi = unit - tile * rows * a.G;
+    const int r = wi / a.G, frame = tile * a.G + (wi - r * a.G);
+    if (frame >= a.nk) return;
+    int p = 0, y = r;
+    if (y >= a.pl[0].rows) { y -= a.pl[0].rows; p = 1; }
+    if (p == 1 && y >= a.pl[1].rows) { y -= a.pl[1].rows; p = 2; }
+    const RowPlane &g = a.pl[p];
     const int si = a.idx[2 * frame], sp = a.idx[2 * frame + 1];
-    const int black = (p ? 128 : 16) << (a.depth - 8);
-    const T *srow = si >= 0 ? reinterpret_cast<const T *>(a.src[p] + si * a.sfs[p] + (int64_t)y * a.sls[p]) : nullptr;
-    T *drow = reinterpret_cast<T *>(a.dst[p] + frame * a.dfs[p] + (int64_t)y * a.dls[p]);
+    const T *srow = si >= 0 ? reinterpret_cast<const T *>(g.src + si * g.sfs + (int64_t)y * g.sls) : nullptr;
+    T *drow = reinterpret_cast<T *>(g.dst + frame * g.dfs + (int64_t)y * g.dls);
     // spinner plane geometry
     const int pw = p ? (a.sw >> a.hs) : a.sw, ph = p ? (a.sh >> a.vs) : a.sh;
     const int px0 = p ? (a.ox >> a.hs) : a.ox, py0 = p ? (a.oy >> a.vs) : a.oy;
     const int64_t ysz = (int64_t)a.sw * a.sh, csz = (int64_t)pw * ph;
-    const uint16_t *sbase = a.spin + (int64_t)sp * a.spin_stride;
-    // layout per spinner frame: Y, Al (sw*sh each), then U, V, Ac (csz each)
     const uint16_t *S = nullptr, *A = nullptr;
     const bool in_rows = sp >= 0 && y >= py0 && y < py0 + ph;
     if (in_rows) {
-        S = p == 0 ? sbase : sbase + 2 * ysz + (p == 2 ? csz : 0);
-        A = p == 0 ? sbase + ysz : sbase + 2 * ysz + 2 * csz;
-        S += (int64_t)(y - py0) * pw;
-        A += (int64_t)(y - py0) * pw;
+        // layout per spinner frame: Y, Al (sw*sh each), then U, V, Ac (csz each)
+        const uint16_t *sbase = a.spin + (int64_t)sp * a.spin_stride;
+        S = (p == 0 ? sbase : sbase + 2 * ysz + (p == 2 ? csz : 0)) + (int64_t)(y - py0) * pw;
+        A = (p == 0 ? sbase + ysz : sbase + 2 * ysz + 2 * csz) + (int64_t)(y - py0) * pw;
     }
-    for (int x = (blockIdx.x * 256 + threadIdx.x) * N; x < W; x += gridDim.x * 256 * N) {
-        T v[N];
-        if (srow && x + N <= W && ((reinterpret_cast<uintptr_t>(srow + x) & 15) == 0)) {
-            *reinterpret_cast<uint4 *>(v) = *reinterpret_cast<const uint4 *>(srow + x);
-        } else {
+    const int chunks = (g.W + N - 1) / N;
+    for (int q0 = threadIdx.x; q0 < chunks; q0 += kRowLanes * kRowUnroll) {
+        uint4 v[kRowUnroll];
 #pragma unroll
-            for (int e = 0; e < N; ++e) v[e] = (srow && x + e < W) ? srow[x + e] : static_cast<T>(black);
+        for (int u = 0; u < kRowUnroll; ++u) {
+            const int q = q0 + u * kRowLanes;
+            if (q < chunks) v[u] = shifted_chunk<T>(srow, q * N, 0, g.W, g.black, g.vec);
         }
-        if (in_rows && x + N > px0 && x < px0 + pw) {
 #pragma unroll
-            for (int e = 0; e < N; ++e) {
-                const int sx = x + e - px0;
-                if (sx >= 0 && sx < pw) {
-                    const int al = A[sx];
-                    v[e] = static_cast<T>((static_cast<int>(v[e]) * (255 - al) + static_cast<int>(S[sx]) * al + 127) / 255);
+        for (int u = 0; u < kRowUnroll; ++u) {
+            const int q = q0 + u * kRowLanes, x = q * N;
+            if (q >= chunks) continue;
+            if (in_rows && x + N > px0 && x < px0 + pw) {
+                T e[N];
+                __builtin_memcpy(e, &v[u], 16);
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    const int sx = x + i - px0;
+                    if (sx >= 0 && sx < pw) {
+                        const int al = A[sx];
+                        e[i] = static_cast<T>((static_cast<int>(e[i]) * (255 - al) + static_cast<int>(S[sx]) * al + 127) / 255);
+                    }
                 }
+                __builtin_memcpy(&v[u], e, 16);
             }
+            put_chunk<T>(drow, x, g.W, g.dvec, v[u]);
         }
-        if (x + N <= W && ((reinterpret_cast<uintptr_t>(drow + x) & 15) == 0)) {
-            *reinterpret_cast<uint4 *>(drow + x) = *reinterpret_cast<const uint4 *>(v);
-        } else {
-#pragma unroll
-            for (int e = 0; e < N; ++e)
-                if (x + e < W) drow[x + e] = v[e];
-        }
+    }
+}
+
+// row-kernel plane geometry from the C-ABI frame descriptors
+inline void row_planes(RowPlane *pl, const FmtInfo &fi, const pp_frames *src, const pp_frames *dst, int nframes,
+                       int sw, int sh, int dw, int dh, int x, int y) {
+    const int es = fi.depth > 8 ? 2 : 1;
+    for (int p = 0; p < 3; ++p) {
+        const int hs = p ? fi.hsub : 0, vs = p ? fi.vsub : 0;
+        RowPlane &g = pl[p];
+        g.src = (const uint8_t *)src->data[p];
+        g.sls = src->linesize[p];
+        g.sfs = src->frame_stride[p];
+        g.dst = (uint8_t *)dst->data[p];
+        g.dls = dst->linesize[p];
+        g.dfs = dst->frame_stride[p];
+        g.W = ceil_rshift(dw, hs);
+        g.rows = ceil_rshift(dh, vs);
+        g.iw = ceil_rshift(sw, hs);
+        g.ih = ceil_rshift(sh, vs);
+        g.ox = x >> hs;
+        g.oy = y >> vs;
+        g.black = (p ? 128 : 16) << (fi.depth - 8);
+        g.vec = !((uintptr_t)g.src & 15) && !(g.sls & 15) && (nframes < 2 || !(g.sfs & 15)) && !((g.ox * es) & 15);
+        g.dvec = !((uintptr_t)g.dst & 15) && !(g.dls & 15) && (nframes < 2 || !(g.dfs & 15));
     }
 }
 
@@ -188,24 +242,16 @@ extern "C" int pp_pad_execute(pp_ctx *ctx, int fmt, int sw, int sh, const pp_fra
     y = (y >> fi.vsub) << fi.vsub;
     if (x + sw > dw || y + sh > dh) PP_FAIL(PP_ERR_INVALID, "input %dx%d at (%d,%d) exceeds %dx%d", sw, sh, x, y, dw, dh);
     if (nframes == 0) return PP_OK;
-    hipStream_t st = static_cast<hipStream_t>(stream);
     PP_HIP(hipSetDevice(ctx->device));
-    for (int p = 0; p < 3; ++p) {
-        const int hs = p ? fi.hsub : 0, vs = p ? fi.vsub : 0;
-        const int W = ceil_rshift(dw, hs), H = ceil_rshift(dh, vs);
-        const int iw = ceil_rshift(sw, hs), ih = ceil_rshift(sh, vs);
-        const int black = (p ? 128 : 16) << (fi.depth - 8);
-        const int N = fi.depth > 8 ? 8 : 16;
-        dim3 grid(std::max(1, (W + 256 * N - 1) / (256 * N)), H, nframes);
-        if (fi.depth > 8)
-            hipLaunchKernelGGL(pad_kernel<2>, grid, dim3(256), 0, st, (const uint8_t *)src->data[p], src->linesize[p],
-                               src->frame_stride[p], iw, ih, (uint8_t *)dst->data[p], dst->linesize[p],
-                               dst->frame_stride[p], W, H, x >> hs, y >> vs, black);
-        else
-            hipLaunchKernelGGL(pad_kernel<1>, grid, dim3(256), 0, st, (const uint8_t *)src->data[p], src->linesize[p],
-                               src->frame_stride[p], iw, ih, (uint8_t *)dst->data[p], dst->linesize[p],
-                               dst->frame_stride[p], W, H, x >> hs, y >> vs, black);
-    }
+    PadArgs a{};
+    row_planes(a.pl, fi, src, dst, nframes, sw, sh, dw, dh, x, y);
+    const int64_t units = (int64_t)nframes * (a.pl[0].rows + a.pl[1].rows + a.pl[2].rows);
+    if (units >= ((int64_t)1 << 31)) PP_FAIL(PP_ERR_UNSUPPORTED, "pad: too many rows in one call");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (fi.depth > 8)
+        hipLaunchKernelGGL(pad_kernel<2>, dim3((unsigned)units), dim3(kRowLanes), 0, st, a);
+    else
+        hipLaunchKernelGGL(pad_kernel<1>, dim3((unsigned)units), dim3(kRowLanes), 0, st, a);
     PP_HIP(hipGetLastError());
     return PP_OK;
 }
@@ -219,17 +265,8 @@ extern "C" int pp_v210_pack(pp_ctx *ctx, int w, int h, const pp_frames *src, con
     if (dst->linesize[0] < stride || (dst->linesize[0] & 15) || ((uintptr_t)dst->data[0] & 15) ||
         (nframes > 1 && (dst->frame_stride[0] & 15)))
         PP_FAIL(PP_ERR_INVALID, "v210 destination must be 16-B aligned with linesize >= %lld", (long long)stride);
-    if (nframes == 0) return PP_OK;
-    PP_HIP(hipSetDevice(ctx->device));
-    const int chunks = (int)(stride / 16);
-    dim3 grid((chunks + 255) / 256, h, nframes);
-    hipLaunchKernelGGL(v210_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(stream),
-                       (const uint8_t *)src->data[0], (const uint8_t *)src->data[1], (const uint8_t *)src->data[2],
-                       src->linesize[0], src->linesize[1], src->linesize[2], src->frame_stride[0],
-                       src->frame_stride[1], src->frame_stride[2], (uint8_t *)dst->data[0], dst->linesize[0],
-                       dst->frame_stride[0], w, chunks);
-    PP_HIP(hipGetLastError());
-    return PP_OK;
+    // yuv422p10le -> v210 is the fused CPVS pass with the canvas = the frame
+    return pp_cpvs_execute(ctx, PP_FMT_YUV422P10LE, w, h, src, w, h, 0, 0, PP_FMT_V210, dst, nframes, stream);
 }
 
 extern "C" int pp_spinner_upload(pp_ctx *ctx, int fmt, const uint8_t *rgba, int n, int sw, int sh) {
@@ -287,19 +324,15 @@ extern "C" int pp_stall_compose(pp_ctx *ctx, int fmt, int w, int h, const pp_fra
     hipStream_t st = static_cast<hipStream_t>(stream);
     PP_HIP(hipSetDevice(ctx->device));
     StallArgs a{};
-    for (int p = 0; p < 3; ++p) {
-        a.src[p] = (const uint8_t *)src->data[p]; a.sls[p] = src->linesize[p]; a.sfs[p] = src->frame_stride[p];
-        a.dst[p] = (uint8_t *)dst->data[p]; a.dls[p] = dst->linesize[p]; a.dfs[p] = dst->frame_stride[p];
-    }
+    row_planes(a.pl, fi, src, dst, nframes, w, h, w, h, 0, 0);
     a.spin = static_cast<const uint16_t *>(ctx->spin_buf);
     const int cw = ctx->spin_w >> fi.hsub, ch = ctx->spin_h >> fi.vsub;
     a.spin_stride = 2 * (int64_t)ctx->spin_w * ctx->spin_h + 3 * (int64_t)cw * ch;
-    a.w = w; a.h = h; a.hs = fi.hsub; a.vs = fi.vsub; a.depth = fi.depth;
+    a.hs = fi.hsub; a.vs = fi.vsub;
     a.sw = need_spin ? ctx->spin_w : 0; a.sh = need_spin ? ctx->spin_h : 0;
     a.ox = ((w - a.sw) / 2) >> fi.hsub << fi.hsub;
     a.oy = ((h - a.sh) / 2) >> fi.vsub << fi.vsub;
-    const int rows = h + 2 * (h >> fi.vsub);
-    const int N = fi.depth > 8 ? 8 : 16;
+    const int rows = a.pl[0].rows + a.pl[1].rows + a.pl[2].rows;
     // frame indices travel in the kernel arguments, 256 output frames per launch
     for (int k0 = 0; k0 < nframes; k0 += 256) {
         const int nk = std::min(256, nframes - k0);
@@ -308,12 +341,17 @@ extern "C" int pp_stall_compose(pp_ctx *ctx, int fmt, int w, int h, const pp_fra
             a.idx[2 * k + 1] = spinner_index[k0 + k];
         }
         StallArgs b = a;
-        for (int p = 0; p < 3; ++p) b.dst[p] += k0 * a.dfs[p];
-        dim3 grid(std::max(1, (w + 256 * N - 1) / (256 * N)), rows, nk);
+        for (int p = 0; p < 3; ++p) b.pl[p].dst += k0 * a.pl[p].dfs;
+        b.nk = nk;
+        // 1080p10 stall frames: G = 1 1.34 ms, 2 1.09-1.12, 3 1.07-1.10, 4 1.12,
+        // 6 1.03-1.05, 8 1.33, 16 1.42, 64 1.55 (power-of-two tiles alias the
+        // frames' rows onto the same HBM channels)
+        b.G = 6;
+        const dim3 grid((unsigned)((nk + b.G - 1) / b.G * b.G * rows));
         if (fi.depth > 8)
-            hipLaunchKernelGGL(stall_kernel<2>, grid, dim3(256), 0, st, b);
+            hipLaunchKernelGGL(stall_kernel<2>, grid, dim3(kRowLanes), 0, st, b);
         else
-            hipLaunchKernelGGL(stall_kernel<1>, grid, dim3(256), 0, st, b);
+            hipLaunchKernelGGL(stall_kernel<1>, grid, dim3(kRowLanes), 0, st, b);
     }
     PP_HIP(hipGetLastError());
     return PP_OK;

@@ -15,18 +15,35 @@ pytestmark = pytest.mark.gpu
 GOLDEN_SPINNER = os.path.join(os.path.dirname(__file__), "golden", "spinner-128-white.png")
 
 
+def _batch(fmt, frames, gpu, dense):
+    """Frames as a pitched FrameBatch (16-B rows: the vector paths) or a dense
+    frame-interleaved one (rows at any byte offset: the sample-by-sample paths)."""
+    import torch
+    from pixpath.frames import FrameBatch
+    if not dense:
+        return FrameBatch.from_numpy(fmt, synth.batch(frames), device=gpu)
+    h, w = frames[0][0].shape
+    b = FrameBatch.interleaved(fmt, w, h, len(frames), device=gpu)
+    planes = synth.batch(frames)
+    for p in range(3):
+        b.planes[p].copy_(torch.from_numpy(np.ascontiguousarray(planes[p])).to(gpu))
+    return b
+
+
 @pytest.mark.parametrize("fmt,sw,sh,dw,dh", [
     (po.YUV420P, 1920, 800, 1920, 1080),       # SRC 3840x1600 -> AVPVS 1920x800, PC CPVS
     (po.YUV422P10LE, 1920, 1012, 1920, 1080),  # 4096x2160 SRC
     (po.YUV420P10LE, 1280, 533, 1280, 800),    # tablet, odd offset rounded to the chroma grid
     (po.YUV422P, 31, 17, 64, 40),
+    (po.YUV422P10LE, 1280, 720, 1920, 1080),   # 16-B aligned shift: vector loads
+    (po.YUV422P10LE, 1276, 700, 1920, 1080),   # ox = 322: unaligned shift
 ])
-def test_pad_matches_oracle(gpu, fmt, sw, sh, dw, dh):
+@pytest.mark.parametrize("dense", [False, True])
+def test_pad_matches_oracle(gpu, fmt, sw, sh, dw, dh, dense):
     from pixpath import ops
-    from pixpath.frames import FrameBatch
     rng = np.random.default_rng(3)
     frames = [synth.noise_frame(rng, fmt, sw, sh) for _ in range(2)]
-    src = FrameBatch.from_numpy(fmt, synth.batch(frames), device=gpu)
+    src = _batch(fmt, frames, gpu, dense)
     out = ops.pad(src, dw, dh).to_numpy()
     for i in range(2):
         ref = po.pad(fmt, frames[i], dw, dh, (dw - sw) // 2, (dh - sh) // 2)
@@ -48,15 +65,16 @@ def test_v210_matches_oracle(gpu, w, h):
         np.testing.assert_array_equal(out[i], po.v210_pack(frames[i]))
 
 
-@pytest.mark.parametrize("fmt", [po.YUV420P, po.YUV422P10LE, po.YUV420P10LE, po.YUV422P])
-def test_stall_compose_matches_oracle(gpu, fmt):
+@pytest.mark.parametrize("fmt,w,h,dense", [
+    (po.YUV420P, 1920, 1080, False), (po.YUV422P10LE, 1920, 1080, False), (po.YUV420P10LE, 1920, 1080, False),
+    (po.YUV422P, 1920, 1080, False), (po.YUV420P, 202, 170, True), (po.YUV422P10LE, 330, 132, True),
+])
+def test_stall_compose_matches_oracle(gpu, fmt, w, h, dense):
     from pixpath import ops, spinner
-    from pixpath.frames import FrameBatch
     anim, _ = spinner.load_apng(GOLDEN_SPINNER)
-    w, h = 1920, 1080
     rng = np.random.default_rng(404)
     frames = [synth.noise_frame(rng, fmt, w, h) for _ in range(3)]
-    src = FrameBatch.from_numpy(fmt, synth.batch(frames), device=gpu)
+    src = _batch(fmt, frames, gpu, dense)
     ops.spinner_upload(anim, fmt)
     src_idx = np.array([2, 2, -1, 0, 1], np.int32)
     sp_idx = np.array([0, 5, 7, -1, 3], np.int32)
@@ -77,7 +95,8 @@ def test_stall_compose_matches_oracle(gpu, fmt):
     (po.YUV420P, 1920, 800, 1920, 1080), (po.YUV420P, 1920, 1080, 1920, 1080), (po.YUV422P, 1920, 1012, 1920, 1080),
     (po.YUV420P10LE, 1920, 1080, 1920, 1080), (po.YUV420P10LE, 1920, 800, 1920, 1080),
     (po.YUV422P10LE, 1920, 1080, 1920, 1080), (po.YUV422P10LE, 1280, 534, 1280, 720), (po.YUV420P10LE, 100, 38, 100, 50),
-    (po.YUV420P, 102, 38, 102, 50),
+    (po.YUV420P, 102, 38, 102, 50), (po.YUV420P, 1280, 720, 1920, 1080), (po.YUV422P10LE, 1276, 716, 1920, 1080),
+    (po.YUV420P10LE, 1276, 716, 1920, 1080),
 ])
 @pytest.mark.parametrize("content", ["legal", "checker", "noise"])
 def test_fused_cpvs_matches_chain(gpu, fmt, w, h, W, H, content):
@@ -95,6 +114,28 @@ def test_fused_cpvs_matches_chain(gpu, fmt, w, h, W, H, content):
     out = ops.cpvs(src, W, H).to_numpy()[0]
     depth = po.fmt_info(fmt)[0]
     for i in range(2):
+        padded = po.pad(fmt, frames[i], W, H, (W - w) // 2, (H - h) // 2)
+        if depth == 8:
+            (ref,) = po.scale(fmt, padded, po.UYVY422, W, H)
+        else:
+            p422 = padded if fmt == po.YUV422P10LE else po.scale(fmt, padded, po.YUV422P10LE, W, H)
+            ref = po.v210_pack(p422)
+        np.testing.assert_array_equal(out[i], ref)
+
+
+@pytest.mark.parametrize("fmt,w,h,W,H", [
+    (po.YUV420P, 102, 38, 102, 50), (po.YUV420P10LE, 100, 38, 100, 50), (po.YUV422P10LE, 330, 132, 336, 140),
+    (po.YUV422P, 202, 100, 210, 104),
+])
+def test_fused_cpvs_dense_rows(gpu, fmt, w, h, W, H):
+    """Source rows at arbitrary byte offsets (a dense frame-interleaved batch): the
+    sample-by-sample staging path gives the same bytes as the oracle chain."""
+    from pixpath import ops
+    rng = np.random.default_rng(81)
+    frames = [synth.noise_frame(rng, fmt, w, h) for _ in range(3)]
+    out = ops.cpvs(_batch(fmt, frames, gpu, True), W, H).to_numpy()[0]
+    depth = po.fmt_info(fmt)[0]
+    for i in range(3):
         padded = po.pad(fmt, frames[i], W, H, (W - w) // 2, (H - h) // 2)
         if depth == 8:
             (ref,) = po.scale(fmt, padded, po.UYVY422, W, H)

@@ -26,3 +26,25 @@ for f in ['/tmp/strip_u16.s', '/tmp/strip_u8.s']:
         bad += (vs > 0)
 print("instances with VGPR spills:", bad)
 PY
+# every kernel of every HIP source: no private (scratch) segment
+for f in scale cpvs pack siti; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -x hip csrc/$f.hip --cuda-device-only -S -o /tmp/$f.s 2>/dev/null &
+done
+wait
+python3 - <<'PY'
+import re
+bad = []
+for f in ['scale', 'cpvs', 'pack', 'siti', 'strip_u16', 'strip_u8']:
+    txt = open('/tmp/%s.s' % f).read()
+    for b in txt.split('  - .agpr_count:')[1:]:
+        name = re.search(r"\.name:\s+(\S+)", b).group(1)
+        ps = int(re.search(r"\.private_segment_fixed_size:\s+(\d+)", b).group(1))
+        if ps:
+            bad.append((f, name, ps))
+for x in bad:
+    print("scratch: %s %s %d B" % x)
+print("kernels with a private segment:", len(bad))
+PY
+# v_ashr_pk_u8_i32 keeps its destination's high half: a kernel that ORs more bytes
+# into such a result is wrong (cpvs.hip hit this); flag every occurrence
+grep -l "v_ashr_pk_u8_i32" /tmp/scale.s /tmp/cpvs.s /tmp/pack.s /tmp/siti.s /tmp/strip_u16.s /tmp/strip_u8.s && echo "v_ashr_pk_u8_i32 present: check its uses" || echo "no v_ashr_pk_u8_i32"
