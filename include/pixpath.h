@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PP_ABI_VERSION 1
+#define PP_ABI_VERSION 2
 
 /* return codes */
 #define PP_OK 0
@@ -172,6 +172,40 @@ int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma,
  * output frames (<= capacity) or <0. */
 int pp_fps_map(int n_in, int64_t in_num, int64_t in_den, int64_t out_num,
                int64_t out_den, int32_t *map, int capacity);
+
+/* ---- host transfer: device / pinned host memory, streams, events, copies --
+ * SURVEY.md 8(b) "pinned host alloc + async H2D/D2H on caller-supplied
+ * streams": everything a host without torch needs between ffmpeg's decode
+ * pipe and its encode pipe (the reference hands frames between decoder,
+ * filter graph and encoder inside one ffmpeg process, lib/ffmpeg.py:992-998).
+ * Streams and events are hipStream_t / hipEvent_t passed as void*.  The
+ * caller owns every buffer it allocates here and frees it with the matching
+ * call. */
+#define PP_COPY_H2D 1
+#define PP_COPY_D2H 2
+#define PP_COPY_D2D 3
+int pp_device_alloc(pp_ctx *ctx, int64_t bytes, void **out);
+int pp_device_free(pp_ctx *ctx, void *ptr);
+int pp_host_alloc(int64_t bytes, void **out);   /* page-locked (pinned) */
+int pp_host_free(void *ptr);
+int pp_stream_create(pp_ctx *ctx, void **out);  /* non-blocking stream */
+int pp_stream_destroy(pp_ctx *ctx, void *stream);
+int pp_stream_synchronize(void *stream);
+int pp_event_create(pp_ctx *ctx, void **out);
+int pp_event_destroy(void *event);
+int pp_event_record(void *event, void *stream);
+int pp_stream_wait_event(void *stream, void *event);
+int pp_event_synchronize(void *event);
+int pp_event_elapsed_ms(void *start, void *end, float *ms);
+/* `bytes` contiguous bytes; kind PP_COPY_*. */
+int pp_copy_async(void *dst, const void *src, int64_t bytes, int kind, void *stream);
+/* `rows` rows of `width_bytes`, pitches in bytes. */
+int pp_copy2d_async(void *dst, int64_t dpitch, const void *src, int64_t spitch,
+                    int64_t width_bytes, int64_t rows, int kind, void *stream);
+/* All planes of `nframes` w x h frames of `fmt` between two pp_frames layouts
+ * (e.g. a dense pinned host batch and a pitched device batch). */
+int pp_frames_copy_async(int fmt, int w, int h, const pp_frames *dst,
+                         const pp_frames *src, int nframes, int kind, void *stream);
 
 #ifdef __cplusplus
 }

@@ -18,7 +18,12 @@ EXPORTS = (
     "pp_v210_linesize", "pp_scale_plan_create", "pp_scale_plan_destroy", "pp_scale_plan_filter",
     "pp_scale_plan_path", "pp_scale_plan_stats", "pp_scale_execute", "pp_pad_execute", "pp_v210_pack", "pp_cpvs_execute", "pp_spinner_upload", "pp_stall_compose",
     "pp_siti", "pp_fps_map",
+    "pp_device_alloc", "pp_device_free", "pp_host_alloc", "pp_host_free", "pp_stream_create",
+    "pp_stream_destroy", "pp_stream_synchronize", "pp_event_create", "pp_event_destroy", "pp_event_record",
+    "pp_stream_wait_event", "pp_event_synchronize", "pp_event_elapsed_ms", "pp_copy_async", "pp_copy2d_async",
+    "pp_frames_copy_async",
 )
+PP_COPY_H2D, PP_COPY_D2H, PP_COPY_D2D = 1, 2, 3
 
 
 class NativeMissing(RuntimeError):
@@ -70,6 +75,22 @@ def lib():
         "pp_stall_compose": (i32, [vp, i32, i32, i32, fr, vp, vp, fr, i32, vp]),
         "pp_siti": (i32, [vp, i32, i32, i32, vp, i64, i64, i32, vp, vp, vp, vp]),
         "pp_fps_map": (i32, [i32, i64, i64, i64, i64, vp, i32]),
+        "pp_device_alloc": (i32, [vp, i64, ctypes.POINTER(vp)]),
+        "pp_device_free": (i32, [vp, vp]),
+        "pp_host_alloc": (i32, [i64, ctypes.POINTER(vp)]),
+        "pp_host_free": (i32, [vp]),
+        "pp_stream_create": (i32, [vp, ctypes.POINTER(vp)]),
+        "pp_stream_destroy": (i32, [vp, vp]),
+        "pp_stream_synchronize": (i32, [vp]),
+        "pp_event_create": (i32, [vp, ctypes.POINTER(vp)]),
+        "pp_event_destroy": (i32, [vp]),
+        "pp_event_record": (i32, [vp, vp]),
+        "pp_stream_wait_event": (i32, [vp, vp]),
+        "pp_event_synchronize": (i32, [vp]),
+        "pp_event_elapsed_ms": (i32, [vp, vp, ctypes.POINTER(ctypes.c_float)]),
+        "pp_copy_async": (i32, [vp, vp, i64, i32, vp]),
+        "pp_copy2d_async": (i32, [vp, i64, vp, i64, i64, i64, i32, vp]),
+        "pp_frames_copy_async": (i32, [i32, i32, i32, fr, fr, i32, i32, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

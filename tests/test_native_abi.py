@@ -25,7 +25,25 @@ def test_library_exports_every_declared_symbol():
     assert declared == set(_native.EXPORTS)
     for name in declared:
         assert hasattr(L, name)
-    assert L.pp_abi_version() == 1
+    assert L.pp_abi_version() == 2
+
+
+def test_host_transfer_argument_checks():
+    """The host-transfer entry points validate before touching HIP: bad sizes,
+    kinds and pitches are PP_ERR_INVALID with a message (no GPU needed)."""
+    L = _native.lib()
+    buf = (ctypes.c_uint8 * 64)()
+    assert L.pp_copy_async(buf, buf, -1, _native.PP_COPY_H2D, None) == -1
+    assert L.pp_copy_async(buf, buf, 8, 7, None) == -1
+    assert b"kind" in L.pp_last_error()
+    assert L.pp_copy2d_async(buf, 4, buf, 8, 8, 2, _native.PP_COPY_D2D, None) == -1
+    assert b"pitch" in L.pp_last_error()
+    assert L.pp_copy_async(None, None, 0, _native.PP_COPY_D2H, None) == 0
+    out = ctypes.c_void_p()
+    assert L.pp_device_alloc(None, 16, ctypes.byref(out)) == -1
+    assert L.pp_host_alloc(-5, ctypes.byref(out)) == -1
+    assert L.pp_frames_copy_async(99, 8, 8, ctypes.byref(_native.pp_frames()), ctypes.byref(_native.pp_frames()),
+                                  1, 1, None) == -1
 
 
 def test_no_gpu_fails_loudly():
