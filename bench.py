@@ -67,7 +67,7 @@ def frame_bytes(fmt, w, h):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30)  # ~2 s timed at 1 GPU: long enough for a busy sampler to see the GPU
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=FRAMES, help="frames per PVS")
     ap.add_argument("--pvs-per-rank", type=int, default=32)

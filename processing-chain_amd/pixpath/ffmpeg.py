@@ -13,7 +13,8 @@ PIXPATH_BACKEND:
   ``python3 -m pixpath.cli`` (ffmpeg still decodes and encodes; frames cross
   PCIe once each way and every filter between decode and encode runs as HIP
   kernels).  Builders without pixel work (stream-copy concat, audio mux,
-  preview) and the x264-encoded mobile/tablet CPVS keep their ffmpeg strings.
+  preview) keep their ffmpeg strings; the mobile/tablet CPVS run their scale on
+  the MI355X and keep x264 (the tablet pad branch keeps the reference's string).
 
 Reference functions mirrored (file:line in pnats2avhd/processing-chain):
   calculate_avpvs_video_dimensions  lib/ffmpeg.py:33
@@ -372,7 +373,20 @@ def create_cpvs(pvs, post_processing, rawvideo=False, overwrite=False, nonraw_cr
             total_duration = str(pvs.hrc.get_long_hrc_duration())
             aformat_normalize = "-c:a aac -b:a 512k"
             mobile_aopts = "-c:a aac -b:a 512k -t {total_duration}".format(**locals())
-        cmd = simple_encoding(pvs, overwrite, input_file, output_file, mobile_vopts, mobile_aopts, filters)
+        if _backend == "gpu" and filters.startswith("-filter:v 'scale="):
+            # `scale=DW:DH:flags=bicubic,setsar=1/1` into libx264's yuv420p: ffmpeg
+            # negotiates one swscale context (resize + conversion), i.e. one plan on
+            # the MI355X; the same x264 options encode the piped frames.  The pad
+            # branch above keeps the reference's string (its leading comma makes
+            # ffmpeg reject the graph, lib/ffmpeg.py:1206-1210; so does the drop-in).
+            overwrite_spec, skip = _skip_existing(output_file, overwrite)
+            if skip:
+                return None
+            cmd = _collapse(_gpu_cli("avpvs", [overwrite_spec, "--input", input_file, "--size", "%dx%d" % (
+                post_processing.display_width, post_processing.display_height), "--flags", "bicubic",
+                "--pix-fmt", "yuv420p", "--vopts", mobile_vopts, "--aopts", mobile_aopts, output_file]))
+        else:
+            cmd = simple_encoding(pvs, overwrite, input_file, output_file, mobile_vopts, mobile_aopts, filters)
 
     if test_config.is_long():
         if cmd is None:

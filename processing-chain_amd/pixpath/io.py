@@ -188,7 +188,7 @@ class FFmpegWriter(Writer):  # pragma: no cover - needs ffmpeg
     """Encode raw frames with the reference's encoder options (e.g. FFV1 / v210 / rawvideo)."""
 
     def __init__(self, path, f, w, h, rate, vopts, aopts="-an", audio_from=None, overwrite="-y", extra_in="",
-                 audio_filter=None):
+                 audio_filter=None, sar="1/1"):
         r = Fraction(rate)
         cmd = "ffmpeg -nostdin -v error {ow} -f rawvideo -pix_fmt {pf} -s {w}x{h} -r {num}/{den} -i pipe:0 ".format(
             ow=overwrite, pf=formats.fmt(f).name if not formats.fmt(f).packed else
@@ -199,7 +199,10 @@ class FFmpegWriter(Writer):  # pragma: no cover - needs ffmpeg
                                                                           shlex.quote(audio_filter))
         elif audio_from:
             cmd += "-i {} -map 0:v -map 1:a? ".format(shlex.quote(audio_from))
-        cmd += "{} {} {} {}".format(extra_in, vopts, aopts, shlex.quote(path))
+        # a raw pipe carries no sample aspect ratio: restate the 1:1 the reference's
+        # chains set (setsar=1/1, lib/ffmpeg.py:992, :1038, :1213) or inherit
+        sar_opt = "-filter:v setsar={}".format(sar) if sar else ""
+        cmd += "{} {} {} {} {}".format(extra_in, sar_opt, vopts, aopts, shlex.quote(path))
         self.proc = subprocess.Popen(cmd, shell=True, stdin=subprocess.PIPE, bufsize=1 << 24)
 
     def write(self, frames_u8):

@@ -50,6 +50,25 @@ def test_cli_avpvs_short_with_fps(gpu, tmp_path):
     assert os.path.getmtime(out) == mtime
 
 
+def test_cli_mobile_cpvs_scale(gpu, tmp_path):
+    """create_cpvs mobile branch (gpu backend): `scale=1280:720:flags=bicubic` into
+    x264's yuv420p as ONE swscale context (resize + 10->8-bit 4:2:2->4:2:0 with
+    ffmpeg's ordered dither) -- what `cli avpvs --pix-fmt yuv420p` runs."""
+    from pixpath import cli
+    rng = np.random.default_rng(5)
+    frames = [synth.noise_frame(rng, po.YUV422P10LE, 1920, 1080) for _ in range(5)]
+    src, out = str(tmp_path / "avpvs.y4m"), str(tmp_path / "mobile.y4m")
+    _write_y4m(src, "yuv422p10le", frames, 1920, 1080)
+    assert cli.main(["avpvs", "-y", "--input", src, "--size", "1280x720", "--flags", "bicubic", "--pix-fmt",
+                     "yuv420p", out]) == 0
+    got = _read(out)
+    assert got[0].shape == (5, 720, 1280)
+    for j in range(5):
+        ref = po.scale(po.YUV422P10LE, frames[j], po.YUV420P, 1280, 720, po.SWS_BICUBIC)
+        for p in range(3):
+            np.testing.assert_array_equal(got[p][j], ref[p])
+
+
 def test_cli_avpvs_segment_canvas(gpu, tmp_path):
     """create_avpvs_segment: scale to the overlay's yuv420p, then -pix_fmt yuv422p10le, canvas of D*R frames
     with the last frame repeated (overlay eof_action=repeat)."""

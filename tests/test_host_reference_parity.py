@@ -208,3 +208,32 @@ def test_gpu_backend_strings(tmp_path):
         assert pff.create_avpvs_short(pvs2, overwrite=False) is None
     finally:
         pff.set_backend("ffmpeg")
+
+
+def test_gpu_backend_mobile_tablet_cpvs():
+    """create_cpvs mobile/tablet (lib/ffmpeg.py:1202-1231), gpu backend: the
+    `scale=DW:DH:flags=bicubic` branch runs `cli avpvs` into yuv420p with the
+    reference's own x264 options; the pad branch (leading comma, rejected by
+    ffmpeg) keeps the reference's string exactly."""
+    seen = set()
+    for sc, want, _ in FX["builders"]:
+        if sc["fn"] != "create_cpvs" or sc["pps"][0][0] not in ("mobile", "tablet"):
+            continue
+        tc, pvs, pps = ref_stubs.build(sc, "/db", Methods)
+        pff.set_backend("gpu")
+        try:
+            got = pff.create_cpvs(pvs, pps[sc.get("pp", 0)], **sc.get("kwargs", {}))
+        finally:
+            pff.set_backend("ffmpeg")
+        if "',pad=" in want:
+            assert got == want
+            seen.add("pad")
+        else:
+            assert "-m pixpath.cli avpvs" in got and "--pix-fmt yuv420p" in got and "--flags bicubic" in got
+            dw, dh = sc["pps"][0][1:3]
+            assert "--size %dx%d" % (dw, dh) in got
+            vo = want[want.index("-c:v libx264"):want.index("faststart") + len("faststart")]
+            assert vo in got  # the reference's x264 options, verbatim
+            assert got.split()[-1] == want.split()[-1]
+            seen.add("scale")
+    assert seen == {"pad", "scale"}
