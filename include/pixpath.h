@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PP_ABI_VERSION 2
+#define PP_ABI_VERSION 3
 
 /* return codes */
 #define PP_OK 0
@@ -206,6 +206,22 @@ int pp_copy2d_async(void *dst, int64_t dpitch, const void *src, int64_t spitch,
  * (e.g. a dense pinned host batch and a pitched device batch). */
 int pp_frames_copy_async(int fmt, int w, int h, const pp_frames *dst,
                          const pp_frames *src, int nframes, int kind, void *stream);
+
+/* ---- p02 byte scanners (host only, no device work) -----------------------
+ * Per-frame sizes of a bitstream held in host memory, exactly as
+ * lib/get_framesize.py computes them, quirks included (see csrc/scan.cpp).
+ * Return the number of frames (sizes[] receives the first `cap` of them) or
+ * a negative PP_ERR_*.  pp_annexb_frame_sizes replaces the byte loops of
+ * get_framesize_h264 (lib/get_framesize.py:144-201, PP_NAL_H264) and
+ * get_framesize_h265 (:204-263, PP_NAL_H265) over the *_tmp.h264/.h265 file;
+ * an H.264 NAL header on which the reference raises ValueError (hex digit
+ * a..f, :180) returns PP_ERR_INVALID.  pp_ivf_frame_sizes replaces
+ * get_framesize_vp9's IVF walk (:87-141); *misdetected counts the frames whose
+ * header fails the "10" frame-marker test (the reference prints a line each). */
+#define PP_NAL_H264 1
+#define PP_NAL_H265 2
+int64_t pp_annexb_frame_sizes(const uint8_t *buf, int64_t n, int codec, int64_t *sizes, int64_t cap);
+int64_t pp_ivf_frame_sizes(const uint8_t *buf, int64_t n, int64_t *sizes, int64_t cap, int64_t *misdetected);
 
 #ifdef __cplusplus
 }

@@ -21,9 +21,10 @@ EXPORTS = (
     "pp_device_alloc", "pp_device_free", "pp_host_alloc", "pp_host_free", "pp_stream_create",
     "pp_stream_destroy", "pp_stream_synchronize", "pp_event_create", "pp_event_destroy", "pp_event_record",
     "pp_stream_wait_event", "pp_event_synchronize", "pp_event_elapsed_ms", "pp_copy_async", "pp_copy2d_async",
-    "pp_frames_copy_async",
+    "pp_frames_copy_async", "pp_annexb_frame_sizes", "pp_ivf_frame_sizes",
 )
 PP_COPY_H2D, PP_COPY_D2H, PP_COPY_D2D = 1, 2, 3
+PP_NAL_H264, PP_NAL_H265 = 1, 2
 
 
 class NativeMissing(RuntimeError):
@@ -91,6 +92,8 @@ def lib():
         "pp_copy_async": (i32, [vp, vp, i64, i32, vp]),
         "pp_copy2d_async": (i32, [vp, i64, vp, i64, i64, i64, i32, vp]),
         "pp_frames_copy_async": (i32, [i32, i32, i32, fr, fr, i32, i32, vp]),
+        "pp_annexb_frame_sizes": (i64, [vp, i64, i32, vp, i64]),
+        "pp_ivf_frame_sizes": (i64, [vp, i64, vp, i64, ctypes.POINTER(i64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
