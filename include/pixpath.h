@@ -113,6 +113,18 @@ int pp_scale_plan_path(const pp_scale_plan *plan);
  * luma staged columns, luma window rows, luma max new rows per chunk}.
  * Returns the number of values written. */
 int pp_scale_plan_stats(const pp_scale_plan *plan, int64_t *out, int n);
+/* The two-stage chain of create_avpvs_segment (lib/ffmpeg.py:1037-1048):
+ * `scale=W:H:flags=...` into the overlay's yuv420p, then libavfilter's
+ * auto-inserted yuv420p -> dst_fmt conversion at the same size (bicubic).
+ * Executed with pp_scale_execute; bit-exact with running the two plans one
+ * after the other.  When the first stage is a strip plan
+ * (pp_scale_plan_path > 0) both stages run in ONE kernel launch with no
+ * intermediate in HBM; otherwise two launches through a plan-owned yuv420p
+ * scratch batch (so such a plan serves one stream at a time).
+ * dst_fmt: yuv420p (one stage), yuv422p, yuv420p10le, yuv422p10le. */
+int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int src_w, int src_h,
+                               int dst_fmt, int dst_w, int dst_h, int flags,
+                               double param0, double param1, pp_scale_plan **out);
 /* Run the plan on `nframes` device frames. */
 int pp_scale_execute(pp_scale_plan *plan, const pp_frames *src,
                      const pp_frames *dst, int nframes, void *stream);

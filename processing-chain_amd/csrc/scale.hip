@@ -412,7 +412,7 @@ inline int ht_bucket(int t) {
 
 // ---------------------------------------------------------------------------
 struct pp_scale_plan {
-    enum Kind { GENERIC, COPY, INTERLEAVE, GENERIC_UYVY } kind = GENERIC;
+    enum Kind { GENERIC, COPY, INTERLEAVE, GENERIC_UYVY, CHAIN } kind = GENERIC;
     pp_ctx *ctx = nullptr;
     int src_fmt = 0, dst_fmt = 0, sw = 0, sh = 0, dw = 0, dh = 0;
     pp::FmtInfo si{}, di{};
@@ -427,6 +427,13 @@ struct pp_scale_plan {
     pp::PlaneJob fjob[3]{}; // strip_kernel jobs (fast_hw > 0)
     int fast_hw = 0;        // H window dwords of strip_kernel, 0 = generic kernel only
     size_t fast_lds = 0;
+    // CHAIN (pp_scale_chain_plan_create): this plan is the first stage (-> yuv420p)
+    pp_scale_plan *stage2 = nullptr;  // yuv420p -> target at the same size (two-launch path)
+    int chain_out = 0;                // target bit depth
+    Kind first_kind = GENERIC;        // the first stage's own kind (two-launch path)
+    bool chain_fused = false;         // one strip_kernel launch does both stages
+    size_t chain_lds = 0;
+    void *dev2 = nullptr;             // second-stage tables (vrow2, chunk2)
 };
 
 namespace {
@@ -542,13 +549,13 @@ static size_t lds_budget() {
 
 // Strip width / chunk height / segments for one plane: the widest strip and
 // tallest chunk whose LDS (staging + ring) fits the budget; ~256-row segments.
-int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::string *err) {
+int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::string *err, int seg_force = 0) {
     static const int tws[] = {256, 128, 64, 32};
     static const int chos[] = {64, 48, 32, 24, 16, 8, 4, 2, 1};
     // tuning overrides (measurement only): tallest chunk, rows per segment
     const char *e_cho = std::getenv("PIXPATH_SCALE_CHO_MAX"), *e_seg = std::getenv("PIXPATH_SCALE_SEG_ROWS");
     const int cho_max = e_cho ? std::max(1, atoi(e_cho)) : pp::kChoMax;
-    const int seg_rows = e_seg ? std::max(1, atoi(e_seg)) : pp::kSegRows;
+    const int seg_rows = seg_force > 0 ? seg_force : e_seg ? std::max(1, atoi(e_seg)) : pp::kSegRows;
     for (int tw : tws) {
         if (tw > 32 && tw / 2 >= dw) continue;  // narrower strips suffice for this plane
         const int S = col_windows(hp, sw, dw, tw);
@@ -638,8 +645,10 @@ inline int hw_bucket(int need) {
 
 }  // namespace
 
-extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, int dw, int dh,
-                                    int flags, double p0, double p1, pp_scale_plan **out) {
+// one_seg_chroma: chroma planes walk their whole height in one segment (the
+// chain plan's second-stage vertical filter follows the first stage's rows)
+static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, int dw, int dh, int flags, double p0,
+                       double p1, bool one_seg_chroma, pp_scale_plan **out) {
     using namespace pp;
     if (!out) PP_FAIL(PP_ERR_INVALID, "null argument");
     *out = nullptr;  // ctx == NULL: host-only plan (tables for introspection, no device upload)
@@ -702,7 +711,7 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
         if (hp[c].h.taps != ht && P->f[c].compact(src_w, ht, &hp[c].h, &err))
             PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
         pair_rows(hp[c]);
-        if (plan_tiles(hp[c], src_w, src_h, dst_w, dst_h, &P->lds_bytes, &err))
+        if (plan_tiles(hp[c], src_w, src_h, dst_w, dst_h, &P->lds_bytes, &err, c && one_seg_chroma ? 1 << 20 : 0))
             PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
     }
     // strip_kernel eligibility: 256-column strips, <= 8 V tap pairs, one H window
@@ -732,6 +741,26 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
         }
     }
 
+    // launch geometry of every plane (host-only plans too: introspection, chain planning)
+    {
+        int base = 0;
+        for (int p = 0; p < 3; ++p) {
+            const int c = p ? 1 : 0;
+            PlaneJob &J = P->job[p];
+            J.sw = c ? P->csw : sw; J.sh = c ? P->csh : sh;
+            J.dw = c ? P->cdw : dw; J.dh = c ? P->cdh : dh;
+            J.tiles_x = hp[c].tiles_x; J.tiles_y = hp[c].nseg; J.tw = hp[c].tw;
+            J.twl = 0;
+            while ((1 << J.twl) < J.tw) ++J.twl;
+            J.seg_h = hp[c].seg_h; J.cho = hp[c].cho;
+            J.tile_base = base;
+            base += J.tiles_x * J.tiles_y;
+            J.vtp = hp[c].vtp; J.ring = hp[c].ring; J.maxnew = hp[c].maxnew; J.S = hp[c].S;
+            J.dither_off = p == 2 ? 3 : 0;
+            P->fjob[p] = J;
+            P->fjob[p].S = hp[c].S_fast;
+        }
+    }
     if (!ctx) {
         *out = P.release();
         return PP_OK;
@@ -773,20 +802,9 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
     }
     PP_HIP(hipMemcpy(P->dev, host.data(), total, hipMemcpyHostToDevice));
 
-    int base = 0;
     for (int p = 0; p < 3; ++p) {
         const int c = p ? 1 : 0;
         PlaneJob &J = P->job[p];
-        J.sw = c ? P->csw : sw; J.sh = c ? P->csh : sh;
-        J.dw = c ? P->cdw : dw; J.dh = c ? P->cdh : dh;
-        J.tiles_x = hp[c].tiles_x; J.tiles_y = hp[c].nseg; J.tw = hp[c].tw;
-        J.twl = 0;
-        while ((1 << J.twl) < J.tw) ++J.twl;
-        J.seg_h = hp[c].seg_h; J.cho = hp[c].cho;
-        J.tile_base = base;
-        base += J.tiles_x * J.tiles_y;
-        J.vtp = hp[c].vtp; J.ring = hp[c].ring; J.maxnew = hp[c].maxnew; J.S = hp[c].S;
-        J.dither_off = p == 2 ? 3 : 0;
         J.hpos = dptr32[c][0]; J.hcoef = dptr16[c][0];
         J.vbase = dptr32[c][1]; J.vcoef2 = dptr32[c][6];
         J.tile_c0 = dptr32[c][2]; J.tile_cn = dptr32[c][3];
@@ -799,8 +817,141 @@ extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, in
     return PP_OK;
 }
 
+extern "C" int pp_scale_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, int dw, int dh,
+                                    int flags, double p0, double p1, pp_scale_plan **out) {
+    return plan_create(ctx, src_fmt, sw, sh, dst_fmt, dw, dh, flags, p0, p1, false, out);
+}
+
+namespace {
+
+// An FFmpeg "unscaled" filter bank (initFilter's |xInc - 0x10000| < 10 case):
+// output i takes input i with the single tap `one`.
+bool identity_bank(const pp::FilterBank &f, int one) {
+    for (int i = 0; i < f.n; ++i)
+        for (int j = 0; j < f.size; ++j) {
+            const int16_t c = f.coef[(size_t)i * f.size + j];
+            if (f.pos[i] + j == i ? c != one : c != 0) return false;
+        }
+    return true;
+}
+
+}  // namespace
+
+// create_avpvs_segment's two stages (lib/ffmpeg.py:1037-1048): the scale
+// filter writes the overlay's yuv420p (overlay's default format=yuv420), then
+// libavfilter converts yuv420p -> dst_fmt at the same size with a second
+// swscale context (bicubic).  Both stages in one strip_kernel launch when the
+// first stage is a strip plan and the second stage's luma / horizontal chroma
+// filters are FFmpeg's identity banks (always, for the AVPVS formats).
+extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, int dw, int dh,
+                                          int flags, double p0, double p1, pp_scale_plan **out) {
+    using namespace pp;
+    if (!out) PP_FAIL(PP_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (dst_fmt != PP_FMT_YUV420P && dst_fmt != PP_FMT_YUV422P && dst_fmt != PP_FMT_YUV420P10LE &&
+        dst_fmt != PP_FMT_YUV422P10LE)
+        PP_FAIL(PP_ERR_INVALID, "chain target %d: yuv420p, yuv422p, yuv420p10le or yuv422p10le", dst_fmt);
+    if (dst_fmt == PP_FMT_YUV420P)  // no conversion after the overlay
+        return plan_create(ctx, src_fmt, sw, sh, dst_fmt, dw, dh, flags, p0, p1, false, out);
+    pp_scale_plan *s1 = nullptr, *p2 = nullptr;
+    int rc = plan_create(ctx, src_fmt, sw, sh, PP_FMT_YUV420P, dw, dh, flags, p0, p1, true, &s1);
+    if (rc) return rc;
+    std::unique_ptr<pp_scale_plan> P(s1);
+    rc = plan_create(ctx, PP_FMT_YUV420P, dw, dh, dst_fmt, dw, dh, PP_SWS_BICUBIC, PP_SWS_PARAM_DEFAULT,
+                     PP_SWS_PARAM_DEFAULT, false, &p2);
+    if (rc) return rc;
+    P->first_kind = P->kind;
+    P->kind = pp_scale_plan::CHAIN;
+    P->stage2 = p2;
+    const FmtInfo di = fmt_info(dst_fmt);
+    P->chain_out = di.depth;
+    P->dst_fmt = dst_fmt;
+    if ((p2->kind != pp_scale_plan::GENERIC && p2->kind != pp_scale_plan::COPY) || !P->fast_hw) {
+        *out = P.release();
+        return PP_OK;
+    }
+    const bool v422 = di.vsub == 0;
+    // COPY (yuv420p -> yuv420p10le, planarCopyWrapper) is x << 2 as well
+    bool ok = p2->kind == pp_scale_plan::COPY ||
+              (identity_bank(p2->f[0], 1 << 14) && identity_bank(p2->f[1], 1 << 14) &&
+               identity_bank(p2->f[2], 1 << 12) && (v422 || identity_bank(p2->f[3], 1 << 12)));
+    std::vector<int32_t> vrow2, chunk2;
+    int vtp2 = 0, ring2 = 0;
+    if (ok && v422) {
+        // second-stage chroma rows: compact window, tap pairs, record per row
+        const int cdh1 = P->cdh, dh2 = p2->cdh;
+        HostPlane h2;
+        std::string err;
+        if (p2->f[3].compact(cdh1, 1, &h2.v, &err)) PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
+        pair_rows(h2);
+        vtp2 = h2.vtp;
+        ok = vtp2 <= 4;
+        std::vector<int> need(dh2, 0);
+        vrow2.assign((size_t)dh2 * 16, 0);
+        for (int r = 0; r < dh2; ++r) {
+            int last = 0;
+            for (int k = 0; k < h2.v.taps; ++k)
+                if (h2.v.coef[(size_t)r * h2.v.taps + k]) last = k;
+            need[r] = h2.v.pos[r] + last;
+            vrow2[(size_t)r * 16] = h2.vbase[r];
+            for (int j = 0; j < vtp2 && j < 15; ++j) vrow2[(size_t)r * 16 + 1 + j] = h2.vcoef2[(size_t)r * vtp2 + j];
+        }
+        // per first-stage chunk: the second-stage rows it completes and the ring2 rows kept
+        const int cho = P->fjob[1].cho, nch = (cdh1 + cho - 1) / cho;
+        chunk2.assign((size_t)nch * 4, 0);
+        int done = 0;
+        for (int ci = 0; ci < nch; ++ci) {
+            const int y0 = ci * cho, end = std::min(cdh1, y0 + cho);
+            const int lo2 = done;
+            while (done < dh2 && need[done] < end) ++done;
+            if (ci == nch - 1) done = dh2;
+            const int b2 = (std::min(lo2 < dh2 ? h2.vbase[lo2] : y0, y0)) & ~1;
+            chunk2[4 * ci] = lo2;
+            chunk2[4 * ci + 1] = done;
+            chunk2[4 * ci + 2] = b2;
+            chunk2[4 * ci + 3] = (y0 - b2 + 1) >> 1;
+            int top = end;
+            for (int r = lo2; r < done; ++r) top = std::max(top, h2.vbase[r] + 2 * vtp2);
+            ring2 = std::max(ring2, top - b2);
+        }
+        ring2 = (ring2 + 1) & ~1;
+    }
+    const size_t lds = P->fast_lds + (size_t)ring2 * kTileW * 2;
+    if (!ok || lds > 64 * 1024) {
+        *out = P.release();
+        return PP_OK;
+    }
+    if (!ctx) {  // host-only plan: introspection (pp_scale_plan_path) only
+        P->chain_fused = true;
+        *out = P.release();
+        return PP_OK;
+    }
+    const size_t b1 = (vrow2.size() * 4 + 255) & ~size_t(255), b2 = chunk2.size() * 4;
+    if (v422) {
+        PP_HIP(hipMalloc(&P->dev2, b1 + b2));
+        PP_HIP(hipMemcpy(P->dev2, vrow2.data(), vrow2.size() * 4, hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(static_cast<uint8_t *>(P->dev2) + b1, chunk2.data(), b2, hipMemcpyHostToDevice));
+    }
+    const int widen = P->chain_out > 8 ? 1 : 0;
+    for (int p = 0; p < 3; ++p) {
+        PlaneJob &J = P->fjob[p];
+        J.fuse = (p && v422) ? 2 : widen;
+        if (J.fuse == 2) {
+            J.vtp2 = vtp2;
+            J.vrow2 = static_cast<const int32_t *>(P->dev2);
+            J.chunk2 = reinterpret_cast<const int32_t *>(static_cast<uint8_t *>(P->dev2) + b1);
+        }
+    }
+    P->chain_fused = true;
+    P->chain_lds = lds;
+    *out = P.release();
+    return PP_OK;
+}
+
 extern "C" int pp_scale_plan_destroy(pp_scale_plan *P) {
     if (!P) return PP_OK;
+    if (P->stage2) (void)pp_scale_plan_destroy(P->stage2);
+    if (P->dev2) (void)hipFree(P->dev2);
     if (P->dev) (void)hipFree(P->dev);
     if (P->scratch) (void)hipFree(P->scratch);
     delete P;
@@ -809,6 +960,7 @@ extern "C" int pp_scale_plan_destroy(pp_scale_plan *P) {
 
 extern "C" int pp_scale_plan_path(const pp_scale_plan *P) {
     if (!P) PP_FAIL(PP_ERR_INVALID, "null plan");
+    if (P->kind == pp_scale_plan::CHAIN) return P->chain_fused ? P->fast_hw : 0;
     return (P->kind == pp_scale_plan::GENERIC || P->kind == pp_scale_plan::GENERIC_UYVY) ? P->fast_hw : 0;
 }
 
@@ -894,18 +1046,54 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
     return PP_OK;
 }
 
+// CHAIN, fused: one strip_kernel<.., FUSE = target depth> launch
+int launch_chain(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, int nframes, hipStream_t st) {
+    using namespace pp;
+    ScaleArgs a{};
+    a.nplanes = 3;
+    for (int p = 0; p < 3; ++p) {
+        a.pl[p] = P->fjob[p];
+        a.src[p] = static_cast<const uint8_t *>(src->data[p]);
+        a.sls[p] = src->linesize[p];
+        a.sfs[p] = src->frame_stride[p];
+        a.dst[p] = static_cast<uint8_t *>(dst->data[p]);
+        a.dls[p] = dst->linesize[p];
+        a.dfs[p] = dst->frame_stride[p];
+    }
+    a.hshift = P->si.depth == 8 ? 7 : P->si.depth - 1;
+    a.dither = P->si.depth > 8;
+    a.vec_src = 1;
+    a.vec_dst = 1;
+    for (int p = 0; p < 3; ++p)
+        a.vec_dst &= aligned(a.dst[p], a.dls[p], nframes > 1 ? a.dfs[p] : 0, P->chain_out == 8 ? 4 : 8);
+    const int vtm = strip_vtm_bucket(std::max(P->fjob[0].vtp, P->fjob[1].vtp));
+    KernelFn k = P->si.depth == 8 ? pick_strip_chain_u8(P->chain_out, P->fast_hw, vtm)
+                                  : pick_strip_chain_u16(P->chain_out, P->fast_hw, vtm);
+    if (!k) PP_FAIL(PP_ERR_UNSUPPORTED, "no chain kernel for window %d", P->fast_hw);
+    const int tiles = P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y;
+    a.tiles = tiles;
+    const int fmax = std::max(1, (1 << 30) / tiles);
+    for (int f0 = 0; f0 < nframes; f0 += fmax) {
+        const int nf = std::min(fmax, nframes - f0);
+        ScaleArgs b = a;
+        for (int p = 0; p < 3; ++p) {
+            b.src[p] += f0 * a.sfs[p];
+            b.dst[p] += f0 * a.dfs[p];
+        }
+        hipLaunchKernelGGL(k, dim3(tiles * nf), dim3(kThreads), P->chain_lds, st, b);
+    }
+    PP_HIP(hipGetLastError());
+    return PP_OK;
+}
+
 }  // namespace
 
-extern "C" int pp_scale_execute(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, int nframes,
-                                void *stream) {
+static int execute_kind(pp_scale_plan *P, pp_scale_plan::Kind kind, const pp_frames *src, const pp_frames *dst,
+                        int nframes, void *stream) {
     using namespace pp;
-    if (!P || !src || !dst || nframes < 0) PP_FAIL(PP_ERR_INVALID, "null argument");
-    if (!P->ctx) PP_FAIL(PP_ERR_INVALID, "host-only plan (created without a context) cannot execute");
-    if (nframes == 0) return PP_OK;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    PP_HIP(hipSetDevice(P->ctx->device));
     const int sbytes = P->si.depth > 8 ? 2 : 1;
-    switch (P->kind) {
+    switch (kind) {
     case pp_scale_plan::COPY: {
         const int dbytes = P->di.depth > 8 ? 2 : 1;
         for (int p = 0; p < 3; ++p) {
@@ -930,6 +1118,30 @@ extern "C" int pp_scale_execute(pp_scale_plan *P, const pp_frames *src, const pp
     }
     case pp_scale_plan::GENERIC:
         return launch_generic(P, src, dst, nframes, st, P->di.depth, true);
+    case pp_scale_plan::CHAIN: {
+        bool vsrc = true;
+        for (int p = 0; p < 3; ++p) vsrc &= aligned(src->data[p], src->linesize[p], nframes > 1 ? src->frame_stride[p] : 0, 16);
+        if (P->chain_fused && vsrc) return launch_chain(P, src, dst, nframes, st);
+        // two launches through a yuv420p scratch batch (plan-owned: one stream at a time)
+        const int64_t yb = (int64_t)P->dw * P->dh, cb = (int64_t)P->cdw * P->cdh;
+        const int64_t per = ((yb + 15) & ~int64_t(15)) + 2 * ((cb + 15) & ~int64_t(15));
+        if (P->scratch_frames < nframes) {
+            if (P->scratch) PP_HIP(hipFree(P->scratch));
+            P->scratch = nullptr;
+            P->scratch_frames = 0;
+            PP_HIP(hipMalloc(&P->scratch, per * nframes));
+            P->scratch_frames = nframes;
+        }
+        uint8_t *s = static_cast<uint8_t *>(P->scratch);
+        const int64_t ys = (yb + 15) & ~int64_t(15), cs = (cb + 15) & ~int64_t(15);
+        pp_frames tmp{};
+        tmp.data[0] = s; tmp.data[1] = s + ys * nframes; tmp.data[2] = s + (ys + cs) * nframes;
+        tmp.linesize[0] = P->dw; tmp.linesize[1] = tmp.linesize[2] = P->cdw;
+        tmp.frame_stride[0] = ys; tmp.frame_stride[1] = tmp.frame_stride[2] = cs;
+        const int rc = execute_kind(P, P->first_kind, src, &tmp, nframes, stream);
+        if (rc) return rc;
+        return pp_scale_execute(P->stage2, &tmp, dst, nframes, stream);
+    }
     case pp_scale_plan::GENERIC_UYVY: {
         // yuv2packedX: planar 8-bit 4:2:2 (flat rounding) then interleave
         const int64_t yb = (int64_t)P->dw * P->dh, cb = (int64_t)P->cdw * P->cdh;
@@ -959,4 +1171,13 @@ extern "C" int pp_scale_execute(pp_scale_plan *P, const pp_frames *src, const pp
     }
     }
     PP_FAIL(PP_ERR_INVALID, "bad plan kind");
+}
+
+extern "C" int pp_scale_execute(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, int nframes,
+                                void *stream) {
+    if (!P || !src || !dst || nframes < 0) PP_FAIL(PP_ERR_INVALID, "null argument");
+    if (!P->ctx) PP_FAIL(PP_ERR_INVALID, "host-only plan (created without a context) cannot execute");
+    if (nframes == 0) return PP_OK;
+    PP_HIP(hipSetDevice(P->ctx->device));
+    return execute_kind(P, P->kind, src, dst, nframes, stream);
 }

@@ -27,6 +27,24 @@ static __constant__ uint8_t c_dither[8][8] = {
     {48, 80, 40, 72, 54, 86, 46, 78},  {112, 16, 104, 8, 118, 22, 110, 14},
 };
 
+// the same matrix, one row per 64-bit word (byte k = column k): a wave-uniform
+// row index makes it one scalar load, the lane's 4 columns one rotate
+constexpr uint64_t dither_row64(const uint8_t (&r)[8]) {
+    uint64_t v = 0;
+    for (int k = 7; k >= 0; --k) v = (v << 8) | r[k];
+    return v;
+}
+constexpr uint8_t kDither[8][8] = {
+    {36, 68, 60, 92, 34, 66, 58, 90},  {100, 4, 124, 28, 98, 2, 122, 26},
+    {52, 84, 44, 76, 50, 82, 42, 74},  {116, 20, 108, 12, 114, 18, 106, 10},
+    {32, 64, 56, 88, 38, 70, 62, 94},  {96, 0, 120, 24, 102, 6, 126, 30},
+    {48, 80, 40, 72, 54, 86, 46, 78},  {112, 16, 104, 8, 118, 22, 110, 14},
+};
+static __constant__ uint64_t c_dither64[8] = {
+    dither_row64(kDither[0]), dither_row64(kDither[1]), dither_row64(kDither[2]), dither_row64(kDither[3]),
+    dither_row64(kDither[4]), dither_row64(kDither[5]), dither_row64(kDither[6]), dither_row64(kDither[7]),
+};
+
 struct PlaneJob {
     int sw, sh, dw, dh;
     int tiles_x, tiles_y, tile_base;  // strips x vertical segments, first block index
@@ -43,6 +61,11 @@ struct PlaneJob {
     const int32_t *hbase4;  // [tiles_x * 64] 8-B aligned window base (staged-row sample) per 4-column lane
     const int32_t *hcoefw;  // [tiles_x * 64][4][HW] taps re-laid over the lane's HW dwords (int16 pairs)
     const int32_t *vrow16;  // [dh][16] per output row: window base row (even), then 8 tap pairs (zero padded)
+    // chain plans (strip_kernel FUSE != 0, see strip.hpp)
+    int fuse;               // 0 as is, 1 identity second stage, 2 second-stage vertical filter through ring2
+    int vtp2;               // second-stage V tap pairs (fuse 2)
+    const int32_t *vrow2;   // [dh2][16] second-stage row records (base row, tap pairs)
+    const int32_t *chunk2;  // [nch][4] per chunk: second-stage rows [lo2, hi2), ring2 base row, kept pairs
 };
 
 struct ScaleArgs {
@@ -183,6 +206,9 @@ using KernelFn = void (*)(const ScaleArgs);
 // dwords, VTM = largest V tap-pair count over the planes; nullptr if not built
 KernelFn pick_strip_u16(int outb, int hw, int vtm);
 KernelFn pick_strip_u8(int outb, int hw, int vtm);
+// chain plans: first stage to 8 bit, second stage into `out2` (8/10) bits
+KernelFn pick_strip_chain_u16(int out2, int hw, int vtm);
+KernelFn pick_strip_chain_u8(int out2, int hw, int vtm);
 int strip_vtm_bucket(int vtp);
 
 }  // namespace pp

@@ -44,8 +44,47 @@ constexpr int strip_min_waves() {
     return HW >= 12 ? 3 : (VTM <= 5 && HW <= (OUTB == 10 && SB == 2 ? 6 : 4)) ? 6 : 4;
 }
 
-template <typename ST, int OUTB, int HW, int VTM>
-__global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
+// 4 adjacent outputs of a row at column xo (8-bit bytes or 16-bit samples)
+template <int BITS>
+__device__ inline void store4(uint8_t *drow, int xo, const int o[4], bool vec, int dw) {
+    if constexpr (BITS == 8) {
+        if (vec) {
+            *reinterpret_cast<uint32_t *>(drow + xo) =
+                (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | ((uint32_t)o[3] << 24);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (xo + j < dw) drow[xo + j] = (uint8_t)o[j];
+        }
+    } else {
+        uint16_t *d16 = reinterpret_cast<uint16_t *>(drow);
+        if (vec) {
+            uint2 v;
+            v.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+            v.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+            *reinterpret_cast<uint2 *>(d16 + xo) = v;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (xo + j < dw) d16[xo + j] = (uint16_t)o[j];
+        }
+    }
+}
+
+// FUSE (chain plans, pp_scale_chain_plan_create; register bound for 3 waves per
+// SIMD -- ring2 puts the plan's LDS at ~3 workgroups per CU anyway): 0 = plain plan; 8 / 10 = the
+// two-stage chain of create_avpvs_segment -- this kernel's 8-bit (OUTB == 8)
+// output is the overlay's yuv420p, and the per-plane mode J.fuse applies
+// libavfilter's auto-inserted yuv420p -> target conversion (FUSE-bit output)
+// before anything reaches HBM:
+//   fuse 0: stored as is (8-bit target, identity second stage);
+//   fuse 1: identity second stage into FUSE bits (x << 7 -> yuv2planeX);
+//   fuse 2: chroma 4:2:0 -> 4:2:2: the 8-bit rows go to an LDS ring (ring2,
+//     15-bit intermediates = hScale8To15 of the identity H filter), and after
+//     each chunk the second stage's vertical filter (vrow2, chunk2 tables)
+//     emits every output row whose taps are all in the ring.
+template <typename ST, int OUTB, int HW, int VTM, int FUSE = 0>
+__global__ __launch_bounds__(kThreads, (FUSE ? 3 : strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
     extern __shared__ __align__(16) uint16_t lds[];
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int frame = L / a.tiles;
@@ -67,6 +106,8 @@ __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, H
     const int cx = lane * 4;
     uint16_t *src_t = lds;                                                  // [maxnew][S]
     uint32_t *win = reinterpret_cast<uint32_t *>(lds + J.maxnew * S);       // [ring/2][256] row pairs
+    uint32_t *ring2 = win + (J.ring >> 1) * kTileW;                         // FUSE, fuse 2: [ring2/2][256]
+    const kconst int32_t *chunk2 = as_kconst<int32_t>(J.chunk2);            // [nch][4]: lo2, hi2, base2, keep2
     const ST *sbase = reinterpret_cast<const ST *>(a.src[p] + frame * a.sfs[p]);
     uint8_t *dbase = a.dst[p] + frame * a.dfs[p];
 
@@ -178,10 +219,23 @@ __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, H
         if (more && !(a.debug & 2)) prefetch(pf, nfrom, nhi);
         // kept row pairs move down to the window start, each column by its own
         // lane in increasing order (no lane reads a slot already overwritten)
+        bool moved = false;
         if (shift > 0) {
             for (int k = 0; k < keep; ++k) win[k * kTileW + tid] = win[(k + shift) * kTileW + tid];
-            __syncthreads();
+            moved = true;
         }
+        int base2 = 0;
+        if constexpr (FUSE != 0) {
+            if (J.fuse == 2) {  // ring2 keeps the rows the pending second-stage outputs still read
+                base2 = chunk2[4 * ci + 2];
+                const int shift2 = ci ? (base2 - chunk2[4 * ci - 2]) >> 1 : 0, keep2 = chunk2[4 * ci + 3];
+                if (shift2 > 0) {
+                    for (int k = 0; k < keep2; ++k) ring2[k * kTileW + tid] = ring2[(k + shift2) * kTileW + tid];
+                    moved = true;
+                }
+            }
+        }
+        if (moved) __syncthreads();
         base = nbase;
         // ---- horizontal pass: row pairs of the window, wave-strided ----------
         if (nnew > 0 && (a.debug & 4)) next_src = hi;
@@ -254,10 +308,16 @@ __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, H
                     for (int j = 0; j < VT; ++j) q[j] = rp[j * (kTileW / 4)];
                     int acc[4];
                     if constexpr (OUTB == 8) {
-                        const int drow = y & 7;
+                        // ordered dither: the row's 8 bytes (scalar load, y is wave-uniform)
+                        // rotated to the lane's first column; flat 64 without dither
+                        uint32_t d4 = 0x40404040u;
+                        if (a.dither) {
+                            const uint64_t rv = as_kconst<uint64_t>(c_dither64)[y & 7];
+                            const int rot = ((xo + J.dither_off) & 7) * 8;
+                            d4 = (uint32_t)(rot ? (rv >> rot) | (rv << (64 - rot)) : rv);
+                        }
 #pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            acc[j] = (a.dither ? c_dither[drow][(xo + j + J.dither_off) & 7] : 64) << 12;
+                        for (int j = 0; j < 4; ++j) acc[j] = (int)((d4 >> (8 * j)) & 0xffu) << 12;
                     } else {
 #pragma unroll
                         for (int j = 0; j < 4; ++j) acc[j] = 1 << (10 + 16 - OUTB);
@@ -276,6 +336,25 @@ __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, H
                     int o[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) o[j] = min(max(acc[j] >> sh, 0), mx);
+                    if constexpr (FUSE != 0) {
+                        if (J.fuse == 2) {  // into ring2 (second-stage input), 15-bit
+                            uint16_t *r16 = reinterpret_cast<uint16_t *>(ring2 + ((y - base2) >> 1) * kTileW + cx);
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) r16[2 * j + (y & 1)] = static_cast<uint16_t>(o[j] << 7);
+                            __builtin_amdgcn_sched_barrier(0);
+                            continue;
+                        }
+                        if (J.fuse == 1) {  // identity second stage: one 4096 tap on x << 7
+                            constexpr int r2 = FUSE == 8 ? 64 << 12 : 1 << (10 + 16 - FUSE);
+                            constexpr int s2 = FUSE == 8 ? 19 : 11 + 16 - FUSE;
+                            int w[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) w[j] = ((o[j] << 19) + r2) >> s2;
+                            store4<FUSE>(drow_p, xo, w, lane_full && a.vec_dst, J.dw);
+                            __builtin_amdgcn_sched_barrier(0);
+                            continue;
+                        }
+                    }
                     if constexpr (OUTB == 8) {
                         if (lane_full && a.vec_dst) {
                             *reinterpret_cast<uint32_t *>(drow_p + xo) =
@@ -314,6 +393,38 @@ __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, H
         case 7: if constexpr (VTM >= 7) vpass(std::integral_constant<int, 7>{}); break;
         default: if constexpr (VTM >= 8) vpass(std::integral_constant<int, 8>{}); break;
         }
+        if constexpr (FUSE != 0) {
+            // ---- second stage (fuse 2): vertical filter of the ring2 rows ----
+            if (J.fuse == 2) {
+                __syncthreads();  // this chunk's first-stage rows are in ring2
+                const int lo2 = chunk2[4 * ci], hi2 = chunk2[4 * ci + 1];
+                const kconst int32_t *vrow2 = as_kconst<int32_t>(J.vrow2);
+                const int vtp2 = J.vtp2;
+                for (int r2 = lo2 + wave; r2 < hi2; r2 += 4) {
+                    const kconst int32_t *row = vrow2 + (int64_t)r2 * 16;
+                    const uint4 *rp = reinterpret_cast<const uint4 *>(ring2 + ((row[0] - base2) >> 1) * kTileW + cx);
+                    int acc[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[j] = FUSE == 8 ? 64 << 12 : 1 << (10 + 16 - FUSE);
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        if (jj >= vtp2) break;
+                        const uint4 q = rp[jj * (kTileW / 4)];
+                        const v2i16 c2 = __builtin_bit_cast(v2i16, row[1 + jj]);
+                        acc[0] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.x), c2, acc[0], false);
+                        acc[1] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.y), c2, acc[1], false);
+                        acc[2] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.z), c2, acc[2], false);
+                        acc[3] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.w), c2, acc[3], false);
+                    }
+                    if (!lane_any) continue;
+                    constexpr int s2 = FUSE == 8 ? 19 : 11 + 16 - FUSE;
+                    int w[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) w[j] = min(max(acc[j] >> s2, 0), (1 << FUSE) - 1);
+                    store4<FUSE>(dbase + (int64_t)r2 * dls, xo, w, lane_full && a.vec_dst, J.dw);
+                }
+            }
+        }
         __builtin_amdgcn_s_setprio(0);
     }
 }
@@ -321,24 +432,25 @@ __global__ __launch_bounds__(kThreads, (strip_min_waves<(int)sizeof(ST), OUTB, H
 
 inline int strip_vtm_bucket_impl(int vtp) { return vtp <= 2 ? 2 : vtp <= 3 ? 3 : vtp <= 5 ? 5 : 8; }
 
-#define PP_STRIP_VTM(ST, OUTB, HW)                                           \
+#define PP_STRIP_VTM(ST, OUTB, HW, FUSE)                                     \
     switch (vtm) {                                                           \
-    case 2: return strip_kernel<ST, OUTB, HW, 2>;                            \
-    case 3: return strip_kernel<ST, OUTB, HW, 3>;                            \
-    case 5: return strip_kernel<ST, OUTB, HW, 5>;                            \
-    default: return strip_kernel<ST, OUTB, HW, 8>;                           \
+    case 2: return strip_kernel<ST, OUTB, HW, 2, FUSE>;                      \
+    case 3: return strip_kernel<ST, OUTB, HW, 3, FUSE>;                      \
+    case 5: return strip_kernel<ST, OUTB, HW, 5, FUSE>;                      \
+    default: return strip_kernel<ST, OUTB, HW, 8, FUSE>;                     \
     }
-#define PP_STRIP_HW(ST, OUTB)                                                \
+#define PP_STRIP_HW_F(ST, OUTB, FUSE)                                        \
     switch (hw) {                                                            \
-    case 3: PP_STRIP_VTM(ST, OUTB, 3)                                        \
-    case 4: PP_STRIP_VTM(ST, OUTB, 4)                                        \
-    case 5: PP_STRIP_VTM(ST, OUTB, 5)                                        \
-    case 6: PP_STRIP_VTM(ST, OUTB, 6)                                        \
-    case 8: PP_STRIP_VTM(ST, OUTB, 8)                                        \
-    case 10: PP_STRIP_VTM(ST, OUTB, 10)                                      \
-    case 12: PP_STRIP_VTM(ST, OUTB, 12)                                      \
-    case 16: PP_STRIP_VTM(ST, OUTB, 16)                                      \
+    case 3: PP_STRIP_VTM(ST, OUTB, 3, FUSE)                                  \
+    case 4: PP_STRIP_VTM(ST, OUTB, 4, FUSE)                                  \
+    case 5: PP_STRIP_VTM(ST, OUTB, 5, FUSE)                                  \
+    case 6: PP_STRIP_VTM(ST, OUTB, 6, FUSE)                                  \
+    case 8: PP_STRIP_VTM(ST, OUTB, 8, FUSE)                                  \
+    case 10: PP_STRIP_VTM(ST, OUTB, 10, FUSE)                                \
+    case 12: PP_STRIP_VTM(ST, OUTB, 12, FUSE)                                \
+    case 16: PP_STRIP_VTM(ST, OUTB, 16, FUSE)                                \
     default: return nullptr;                                                 \
     }
+#define PP_STRIP_HW(ST, OUTB) PP_STRIP_HW_F(ST, OUTB, 0)
 
 }  // namespace pp

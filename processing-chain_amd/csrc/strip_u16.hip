@@ -12,4 +12,11 @@ KernelFn pick_strip_u16(int outb, int hw, int vtm) {
 
 int strip_vtm_bucket(int vtp) { return strip_vtm_bucket_impl(vtp); }
 
+KernelFn pick_strip_chain_u16(int out2, int hw, int vtm) {
+    if (out2 == 8) {
+        PP_STRIP_HW_F(uint16_t, 8, 8)
+    }
+    PP_STRIP_HW_F(uint16_t, 8, 10)
+}
+
 }  // namespace pp

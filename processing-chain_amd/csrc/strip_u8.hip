@@ -10,4 +10,11 @@ KernelFn pick_strip_u8(int outb, int hw, int vtm) {
     PP_STRIP_HW(uint8_t, 10)
 }
 
+KernelFn pick_strip_chain_u8(int out2, int hw, int vtm) {
+    if (out2 == 8) {
+        PP_STRIP_HW_F(uint8_t, 8, 8)
+    }
+    PP_STRIP_HW_F(uint8_t, 8, 10)
+}
+
 }  // namespace pp

@@ -15,7 +15,7 @@ ERRORS = {-1: "PP_ERR_INVALID", -2: "PP_ERR_HIP", -3: "PP_ERR_NOMEM", -4: "PP_ER
 # every symbol declared in include/pixpath.h
 EXPORTS = (
     "pp_abi_version", "pp_last_error", "pp_ctx_create", "pp_ctx_destroy", "pp_plane_bytes",
-    "pp_v210_linesize", "pp_scale_plan_create", "pp_scale_plan_destroy", "pp_scale_plan_filter",
+    "pp_v210_linesize", "pp_scale_plan_create", "pp_scale_chain_plan_create", "pp_scale_plan_destroy", "pp_scale_plan_filter",
     "pp_scale_plan_path", "pp_scale_plan_stats", "pp_scale_execute", "pp_pad_execute", "pp_v210_pack", "pp_cpvs_execute", "pp_spinner_upload", "pp_stall_compose",
     "pp_siti", "pp_fps_map",
     "pp_device_alloc", "pp_device_free", "pp_host_alloc", "pp_host_free", "pp_stream_create",
@@ -64,6 +64,7 @@ def lib():
         "pp_plane_bytes": (i64, [i32, i32, i32, i32, i64]),
         "pp_v210_linesize": (i64, [i32]),
         "pp_scale_plan_create": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, dbl, dbl, ctypes.POINTER(vp)]),
+        "pp_scale_chain_plan_create": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, dbl, dbl, ctypes.POINTER(vp)]),
         "pp_scale_plan_destroy": (i32, [vp]),
         "pp_scale_plan_filter": (i32, [vp, i32, vp, vp, i32]),
         "pp_scale_plan_path": (i32, [vp]),

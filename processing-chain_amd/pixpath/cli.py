@@ -100,23 +100,10 @@ def cmd_avpvs(args):
     target = formats.fmt(args.pix_fmt)
     rate = Fraction(args.fps) if args.fps else rd.rate
     if args.overlay_yuv420:
-        # create_avpvs_segment: scale into the overlay's yuv420p, then -pix_fmt conversion
-        s1 = ops.Scaler(rd.fmt, rd.w, rd.h, "yuv420p", W, H, flags=args.flags)
-        s2 = None if target.name == "yuv420p" else ops.Scaler("yuv420p", W, H, target, W, H, flags="bicubic")
-        mid = {}
-
-        def process(src, dst, stream):
-            if s2 is None:
-                s1(src, dst, stream=stream)
-                return
-            n = src.n
-            m = mid.get(n)
-            if m is None:
-                from .frames import FrameBatch
-                m = mid[n] = FrameBatch("yuv420p", W, H, n, device=src.device)
-            s1(src, m, stream=stream)
-            s2(m, dst, stream=stream)
-        stage = Stage(rd.fmt, rd.w, rd.h, target, W, H, process)
+        # create_avpvs_segment: scale into the overlay's yuv420p, then the -pix_fmt
+        # conversion -- one chain plan (a single launch, no yuv420p intermediate)
+        sc = ops.Scaler(rd.fmt, rd.w, rd.h, target, W, H, flags=args.flags, chain=True)
+        stage = Stage(rd.fmt, rd.w, rd.h, target, W, H, lambda s, d, st: sc(s, d, stream=st))
     else:
         sc = ops.Scaler(rd.fmt, rd.w, rd.h, target, W, H, flags=args.flags)
         stage = Stage(rd.fmt, rd.w, rd.h, target, W, H, lambda s, d, st: sc(s, d, stream=st))

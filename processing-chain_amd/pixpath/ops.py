@@ -63,13 +63,17 @@ class Scaler:
     """
 
     def __init__(self, src_fmt, sw, sh, dst_fmt, dw, dh, flags="bicubic", param0=None, param1=None,
-                 device=None):
+                 device=None, chain=False):
+        """chain=True: create_avpvs_segment's two stages (scale into the overlay's
+        yuv420p, then yuv420p -> dst_fmt bicubic at the same size) as one plan
+        (pp_scale_chain_plan_create): one launch when kernel_path > 0."""
         self.src_fmt, self.dst_fmt = formats.fmt(src_fmt), formats.fmt(dst_fmt)
         self.sw, self.sh, self.dw, self.dh = int(sw), int(sh), int(dw), int(dh)
         self.ctx = context(device)
         fl = FLAGS[flags] if isinstance(flags, str) else int(flags)
         h = ctypes.c_void_p()
-        check(lib().pp_scale_plan_create(
+        create = lib().pp_scale_chain_plan_create if chain else lib().pp_scale_plan_create
+        check(create(
             self.ctx.handle, self.src_fmt.id, self.sw, self.sh, self.dst_fmt.id, self.dw, self.dh, fl,
             PARAM_DEFAULT if param0 is None else float(param0),
             PARAM_DEFAULT if param1 is None else float(param1), ctypes.byref(h)))

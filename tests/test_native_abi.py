@@ -117,3 +117,26 @@ def test_fps_map_three_way(n, a, b):
 @pytest.mark.parametrize("w", [1, 6, 47, 48, 49, 1280, 1920, 3840, 4096])
 def test_v210_linesize(w):
     assert _native.lib().pp_v210_linesize(w) == po.v210_linesize(w)
+
+
+@pytest.mark.parametrize("sf,sw,sh,df,dw,dh,fused", [
+    ("yuv420p10le", 1280, 720, "yuv422p10le", 1920, 1080, True),   # config 4 canvas: one launch
+    ("yuv422p10le", 1280, 720, "yuv422p10le", 1920, 1080, True),
+    ("yuv420p", 1280, 720, "yuv422p", 1920, 1080, True),
+    ("yuv420p", 1280, 720, "yuv420p10le", 1920, 1080, True),
+    ("yuv420p", 1920, 1080, "yuv422p10le", 1920, 1080, False),     # unscaled first stage: two launches
+])
+def test_chain_plan_host_only(sf, sw, sh, df, dw, dh, fused):
+    """pp_scale_chain_plan_create (create_avpvs_segment's two stages) decides
+    its launch shape on the host: fused into one strip_kernel launch or two."""
+    L = _native.lib()
+    h = ctypes.c_void_p()
+    _native.check(L.pp_scale_chain_plan_create(None, po.FMT_BY_NAME[sf], sw, sh, po.FMT_BY_NAME[df], dw, dh,
+                                               ops.FLAGS["bicubic"], ops.PARAM_DEFAULT, ops.PARAM_DEFAULT,
+                                               ctypes.byref(h)))
+    try:
+        assert (L.pp_scale_plan_path(h) > 0) == fused
+    finally:
+        L.pp_scale_plan_destroy(h)
+    assert L.pp_scale_chain_plan_create(None, 0, 64, 64, po.FMT_BY_NAME["uyvy422"], 64, 64, 4, 1.0, 1.0,
+                                        ctypes.byref(h)) == -1

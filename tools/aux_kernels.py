@@ -111,6 +111,20 @@ def main():
     ms = timed(lambda: ops.cpvs(s10, dst=dv))
     report("cpvs_v210_420p10_1080p", "cpvs_kernel<10,true>", ms, plane_bytes(s10), plane_bytes(dv),
            "4:2:0 -> 4:2:2 bicubic + v210")
+    del s10, dv
+    # long-test canvas (create_avpvs_segment): 720p yuv420p10le segment -> overlay yuv420p -> yuv422p10le 1080p
+    c720 = filled("yuv420p10le", 1280, 720, n)
+    c1080 = FrameBatch("yuv422p10le", 1920, 1080, n, device=dev)
+    chain = ops.Scaler("yuv420p10le", 1280, 720, "yuv422p10le", 1920, 1080, flags="bicubic", chain=True)
+    ms = timed(lambda: chain(c720, c1080))
+    report("chain_720p10_to_1080p422p10", "strip_kernel<u16,8,..,FUSE=10>" if chain.kernel_path else "two launches",
+           ms, plane_bytes(c720), plane_bytes(c1080), "scale -> yuv420p (dither) -> yuv422p10le in one launch")
+    s1 = ops.Scaler("yuv420p10le", 1280, 720, "yuv420p", 1920, 1080, flags="bicubic")
+    s2 = ops.Scaler("yuv420p", 1920, 1080, "yuv422p10le", 1920, 1080, flags="bicubic")
+    mid = FrameBatch("yuv420p", 1920, 1080, n, device=dev)
+    ms = timed(lambda: (s1(c720, mid), s2(mid, c1080)))
+    report("chain_two_launch_720p10_to_1080p422p10", "strip_kernel + scale_kernel", ms, plane_bytes(c720),
+           plane_bytes(c1080), "round-1 path: yuv420p intermediate in HBM (its bytes not counted)")
     if a.out:
         with open(a.out, "w") as f:
             json.dump(rows, f, indent=1)

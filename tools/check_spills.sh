@@ -13,7 +13,7 @@ for f in ['/tmp/strip_u16.s', '/tmp/strip_u8.s']:
     txt = open(f).read()
     for b in txt.split('  - .agpr_count:')[1:]:
         name = re.search(r"\.name:\s+(\S+)", b).group(1)
-        m = re.search(r"strip_kernelI(\w)Li(\d+)ELi(\d+)ELi(\d+)E", name)
+        m = re.search(r"strip_kernelI(\w)Li(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", name)
         if not m:
             continue
         vg = int(re.search(r"\.vgpr_count:\s+(\d+)", b).group(1))
@@ -22,7 +22,7 @@ for f in ['/tmp/strip_u16.s', '/tmp/strip_u8.s']:
         ss = int(re.search(r"\.sgpr_spill_count:\s+(\d+)", b).group(1))
         st = {'t': 'u16', 'h': 'u8'}[m.group(1)]
         if vs or ss or '-a' in sys.argv:
-            print("%s OUTB=%s HW=%s VTM=%s  vgpr=%d sgpr=%d vspill=%d sspill=%d" % (st, m.group(2), m.group(3), m.group(4), vg, sg, vs, ss))
+            print("%s OUTB=%s HW=%s VTM=%s FUSE=%s  vgpr=%d sgpr=%d vspill=%d sspill=%d" % (st, m.group(2), m.group(3), m.group(4), m.group(5), vg, sg, vs, ss))
         bad += (vs > 0)
 print("instances with VGPR spills:", bad)
 PY
