@@ -549,12 +549,13 @@ static size_t lds_budget() {
 
 // Strip width / chunk height / segments for one plane: the widest strip and
 // tallest chunk whose LDS (staging + ring) fits the budget; ~256-row segments.
-int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::string *err, int seg_force = 0) {
+int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::string *err, int seg_force = 0,
+               int cho_force = 0) {
     static const int tws[] = {256, 128, 64, 32};
     static const int chos[] = {64, 48, 32, 24, 16, 8, 4, 2, 1};
     // tuning overrides (measurement only): tallest chunk, rows per segment
     const char *e_cho = std::getenv("PIXPATH_SCALE_CHO_MAX"), *e_seg = std::getenv("PIXPATH_SCALE_SEG_ROWS");
-    const int cho_max = e_cho ? std::max(1, atoi(e_cho)) : pp::kChoMax;
+    const int cho_max = e_cho ? std::max(1, atoi(e_cho)) : cho_force > 0 ? cho_force : pp::kChoMax;
     const int seg_rows = seg_force > 0 ? seg_force : e_seg ? std::max(1, atoi(e_seg)) : pp::kSegRows;
     for (int tw : tws) {
         if (tw > 32 && tw / 2 >= dw) continue;  // narrower strips suffice for this plane
@@ -648,7 +649,7 @@ inline int hw_bucket(int need) {
 // one_seg_chroma: chroma planes walk their whole height in one segment (the
 // chain plan's second-stage vertical filter follows the first stage's rows)
 static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, int dw, int dh, int flags, double p0,
-                       double p1, bool one_seg_chroma, pp_scale_plan **out) {
+                       double p1, bool one_seg_chroma, pp_scale_plan **out, int cho_max = 0) {
     using namespace pp;
     if (!out) PP_FAIL(PP_ERR_INVALID, "null argument");
     *out = nullptr;  // ctx == NULL: host-only plan (tables for introspection, no device upload)
@@ -711,7 +712,7 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
         if (hp[c].h.taps != ht && P->f[c].compact(src_w, ht, &hp[c].h, &err))
             PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
         pair_rows(hp[c]);
-        if (plan_tiles(hp[c], src_w, src_h, dst_w, dst_h, &P->lds_bytes, &err, c && one_seg_chroma ? 1 << 20 : 0))
+        if (plan_tiles(hp[c], src_w, src_h, dst_w, dst_h, &P->lds_bytes, &err, c && one_seg_chroma ? 1 << 20 : 0, cho_max))
             PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
     }
     // strip_kernel eligibility: 256-column strips, <= 8 V tap pairs, one H window
@@ -837,6 +838,8 @@ bool identity_bank(const pp::FilterBank &f, int one) {
 
 }  // namespace
 
+constexpr int kChainCho = 16;
+
 // create_avpvs_segment's two stages (lib/ffmpeg.py:1037-1048): the scale
 // filter writes the overlay's yuv420p (overlay's default format=yuv420), then
 // libavfilter converts yuv420p -> dst_fmt at the same size with a second
@@ -854,7 +857,10 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
     if (dst_fmt == PP_FMT_YUV420P)  // no conversion after the overlay
         return plan_create(ctx, src_fmt, sw, sh, dst_fmt, dw, dh, flags, p0, p1, false, out);
     pp_scale_plan *s1 = nullptr, *p2 = nullptr;
-    int rc = plan_create(ctx, src_fmt, sw, sh, PP_FMT_YUV420P, dw, dh, flags, p0, p1, true, &s1);
+    // 16-row chunks: the LDS ring of the second stage then still leaves 6
+    // workgroups per CU (32-row chunks: 2.73 vs 2.30 ms per 600-frame config-4
+    // canvas launch, profiles/r2/chain_ab.log)
+    int rc = plan_create(ctx, src_fmt, sw, sh, PP_FMT_YUV420P, dw, dh, flags, p0, p1, true, &s1, kChainCho);
     if (rc) return rc;
     std::unique_ptr<pp_scale_plan> P(s1);
     rc = plan_create(ctx, PP_FMT_YUV420P, dw, dh, dst_fmt, dw, dh, PP_SWS_BICUBIC, PP_SWS_PARAM_DEFAULT,
