@@ -25,10 +25,11 @@
 // sum(d^2) exact in 64-bit integers.  Per (frame, band) partials are written
 // without atomics and reduced in a fixed order by siti_finalize, so results
 // are bit-reproducible.
-// Bound: VALU, not HBM -- the interior frame loop is ~1740 VALU instructions
-// per wave and frame for 8 x 16 pixels a lane (Sobel in packed 16-bit math,
-// one v_sqrt_f32 per pixel, TI by v_dot2), ~73 % VALU-busy at 0.68 ms on
-// config 2 (profiles/r2/siti_experiments.md).
+// Bound: VALU, not HBM -- the interior frame loop is ~1660 VALU instructions
+// per wave and frame for 8 x 16 pixels a lane (per pixel: two op_sel'd
+// v_pk_mad_i16 build (h1, h2), two more give (gx, gy), one v_dot2 |G|^2, one
+// v_sqrt_f32; TI by v_dot2), 0.65 ms on config 2
+// (profiles/r2/siti_experiments.md).
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -107,6 +108,24 @@ __device__ inline uint32_t pk_2a_plus_b(uint32_t a, uint32_t b) {
     asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(0x00020002u), "v"(b));
     return r;
 }
+// v_pk_mad_i16 with half selects: per pixel, the H pass builds the pair
+// R = (right - left, left + 2 centre + right) straight from the packed pixel
+// registers (op_sel broadcasts a half, no v_perm / v_alignbit), and the V pass
+// G = (gx, gy) = Ra * (1, -1) + 2 * Rb.lo + Rc from three rows of R -- so
+// |G|^2 is one v_dot2 of G with itself.  Constants in SGPRs (VOP3P takes no
+// literal on gfx9).
+#define PP_PKMAD(SEL, SELHI)                                                                 \
+    [](uint32_t a, uint32_t b, uint32_t c) {                                                 \
+        uint32_t r;                                                                          \
+        asm("v_pk_mad_i16 %0, %1, %2, %3 op_sel:" SEL " op_sel_hi:" SELHI                    \
+            : "=v"(r) : "v"(a), "s"(b), "v"(c));                                             \
+        return r;                                                                            \
+    }
+constexpr uint32_t kC02 = 0x00020000u;   // (0, 2)
+constexpr uint32_t kCM11 = 0x0001ffffu;  // (-1, 1)
+constexpr uint32_t kC20 = 0x00000002u;   // (2, 0)
+constexpr uint32_t kC1M1 = 0xffff0001u;  // (1, -1)
+
 // gx^2 + gy^2 of one (gx, gy) pair: the VOP3P form with an inline-constant
 // accumulator (the compiler's v_dot2c form needs a zeroed destination copy)
 __device__ inline int sq_norm(v2i16 p) {
@@ -334,28 +353,34 @@ __device__ __forceinline__ void siti_range(const uint8_t *frames, int64_t ls, in
         v2f32 s1 = {0.f, 0.f}, s2 = {0.f, 0.f};
         int d1s = 0;        // |sum d| <= 16 rows * 8 px * 1023
         uint32_t d2s = 0;   // sum d^2 <= 16 * 8 * 1023^2 < 2^32
-        uint32_t h1a[4], h2a[4], h1b[4], h2b[4];  // packed int16 pairs of the rows above
+        uint32_t Ra[kLanePx], Rb[kLanePx];  // (h1, h2) of the two rows above
 #pragma unroll
         for (int ri = 0; ri < NR; ++ri) {
             const int r = y0 - 1 + ri;
+            const bool band = ri >= 1 && ri <= kBand;
+            const int bi = ri - 1;
             uint32_t w[4];
             to_pairs<T>(raw[ri], w);
             // neighbours: the last pixel of the lane below, the first of the lane above
             // (DPP wave shifts; only halo lanes see the wave's ends)
             const uint32_t wl = __builtin_amdgcn_mov_dpp(w[3], 0x138, 0xf, 0xf, true);  // wave_shr:1
             const uint32_t wr = __builtin_amdgcn_mov_dpp(w[0], 0x130, 0xf, 0xf, true);  // wave_shl:1
-            uint32_t h1[4], h2[4];
+            // R[i] = (h1, h2) of pixel i: h1 = right - left, h2 = left + 2 v + right
+            uint32_t R[kLanePx];
+            {
+                const auto mad_t0 = PP_PKMAD("[0,0,1]", "[0,1,1]");  // (v[2k+1], 2 v[2k] + v[2k+1])
+                const auto mad_r0 = PP_PKMAD("[1,0,0]", "[1,1,1]");  // + (-1, 1) * v[2k-1]
+                const auto mad_t1 = PP_PKMAD("[1,0,0]", "[1,1,0]");  // (v[2k+2], 2 v[2k+1] + v[2k+2])
+                const auto mad_r1 = PP_PKMAD("[0,0,0]", "[0,1,1]");  // + (-1, 1) * v[2k]
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                // (v[2k-1], v[2k]) and (v[2k+1], v[2k+2]) as u16 pairs
-                const uint32_t lp = __builtin_amdgcn_alignbit(w[k], k ? w[k - 1] : wl, 16);
-                const uint32_t rp = __builtin_amdgcn_alignbit(k < 3 ? w[k + 1] : wr, w[k], 16);
-                h1[k] = pk_sub(rp, lp);                      // right - left         (|.| <= 1023)
-                h2[k] = pk_add(pk_2a_plus_b(w[k], lp), rp);  // left + 2 v + right (<= 4092)
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t lft = k ? w[k - 1] : wl, rgt = k < 3 ? w[k + 1] : wr;
+                    R[2 * k] = mad_r0(lft, kCM11, mad_t0(w[k], kC02, w[k]));
+                    R[2 * k + 1] = mad_r1(w[k], kCM11, mad_t1(w[k], kC02, rgt));
+                }
             }
             // TI on the band rows against the previous frame's band
-            const int bi = ri - 1;
-            if (ri >= 1 && ri <= kBand) {
+            if (band) {
                 if (INTERIOR || r < y1) {
                     uint32_t q[4];
                     to_pairs<T>(pv[bi], q);
@@ -368,21 +393,24 @@ __device__ __forceinline__ void siti_range(const uint8_t *frames, int64_t ls, in
                         d2s = static_cast<uint32_t>(__builtin_amdgcn_sdot2(d, d, static_cast<int>(d2s), false));
                     }
                 }
-                pv[bi] = raw[ri];
+                pv[bi] = raw[ri];  // (swapping raw/pv roles per frame instead: 178 VGPR spills)
             }
             // Sobel centred on row c = r - 1 (rows c-1, c, c+1 are in the window)
             const int c = r - 1;
             if (ri >= 2 && (INTERIOR || (c < y1 && c >= 1 && c <= H - 2))) {
                 v2f32 mag[4];
+                const auto mad_in = PP_PKMAD("[0,0,0]", "[1,1,1]");
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const uint32_t gx = pk_add(pk_2a_plus_b(h1b[k], h1a[k]), h1[k]);  // |.| <= 4092
-                    const uint32_t gy = pk_sub(h2[k], h2a[k]);
-                    // (gx, gy) of each pixel as one pair: |G|^2 = dot2(p, p)
-                    const v2i16 p0 = __builtin_bit_cast(v2i16, __builtin_amdgcn_perm(gy, gx, 0x05040100u));
-                    const v2i16 p1 = __builtin_bit_cast(v2i16, __builtin_amdgcn_perm(gy, gx, 0x07060302u));
-                    const int g0 = sq_norm(p0), g1 = sq_norm(p1);
-                    mag[k] = v2f32{__fsqrt_rn(static_cast<float>(g0)), __fsqrt_rn(static_cast<float>(g1))};
+                    int g[2];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const int i = 2 * k + e;
+                        // G = (Ra.lo + 2 Rb.lo + Rc.lo, Rc.hi - Ra.hi) = (gx, gy), |.| <= 4092
+                        const uint32_t G = mad_in(Ra[i], kC1M1, mad_in(Rb[i], kC20, R[i]));
+                        g[e] = sq_norm(__builtin_bit_cast(v2i16, G));
+                    }
+                    mag[k] = v2f32{__fsqrt_rn(static_cast<float>(g[0])), __fsqrt_rn(static_cast<float>(g[1]))};
                 }
                 // first valid Sobel row of the band
                 if (INTERIOR ? ri == 2 : (ri == 2 || (ri == 3 && !row2_valid))) {
@@ -402,9 +430,9 @@ __device__ __forceinline__ void siti_range(const uint8_t *frames, int64_t ls, in
                 }
             }
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                h1a[k] = h1b[k]; h2a[k] = h2b[k];
-                h1b[k] = h1[k]; h2b[k] = h2[k];
+            for (int i = 0; i < kLanePx; ++i) {
+                Ra[i] = Rb[i];
+                Rb[i] = R[i];
             }
             // this row is consumed: start loading the next frame's row ri into it
             issue_row<T>(raw[ri], nrs, voff + (uint32_t)r * fls);
