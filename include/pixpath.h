@@ -235,6 +235,26 @@ int pp_frames_copy_async(int fmt, int w, int h, const pp_frames *dst,
 int64_t pp_annexb_frame_sizes(const uint8_t *buf, int64_t n, int codec, int64_t *sizes, int64_t cap);
 int64_t pp_ivf_frame_sizes(const uint8_t *buf, int64_t n, int64_t *sizes, int64_t cap, int64_t *misdetected);
 
+/* ---- FFV1 AVPVS encoder -----------------------
+ * Replaces the `-c:v ffv1 -level 3 -coder 1 -context 1 -slicecrc 1` encode of
+ * the AVPVS (lib/ffmpeg.py:993, :1047): FFV1 version 3 (RFC 9043), range
+ * coder, slice CRCs, every frame a keyframe, slices_h x slices_v slices per
+ * frame (<= 256), one GPU lane per slice.  Bitstream choices and the parity
+ * status (unpinned: no FFV1 decoder exists here) are in DESIGN.md.
+ * pp_ffv1_encoder_create with ctx == NULL builds the configuration record only.
+ * pp_ffv1_extradata copies the configuration record (AVI/MKV codec private
+ * data) and returns its size (cap 0: size only).
+ * pp_ffv1_encode encodes nframes <= max_frames device frames into frame
+ * packets laid out back to back in the device buffer dst (frame_sizes[f] on
+ * the host); it synchronises `stream` and returns the total bytes or < 0. */
+typedef struct pp_ffv1_enc pp_ffv1_enc;
+int pp_ffv1_encoder_create(pp_ctx *ctx, int fmt, int w, int h, int slices_h, int slices_v,
+                           int max_frames, pp_ffv1_enc **out);
+int pp_ffv1_encoder_destroy(pp_ffv1_enc *enc);
+int pp_ffv1_extradata(const pp_ffv1_enc *enc, uint8_t *out, int cap);
+int64_t pp_ffv1_encode(pp_ffv1_enc *enc, const pp_frames *src, int nframes, uint8_t *dst,
+                       int64_t dst_cap, int64_t *frame_sizes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

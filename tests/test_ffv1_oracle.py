@@ -1,0 +1,65 @@
+"""FFV1, host side.
+
+* the CPU restatement (oracle/ffv1_oracle.c) decodes its own packets back to
+  the input losslessly -- 8/10-bit, 4:2:0/4:2:2, noise / smooth / full-range
+  extremes, several slice grids -- including FFmpeg's end-of-slice position
+  check and the slice / record CRCs (the only pinning available: no FFV1
+  decoder exists here, so parity against FFmpeg is unpinned);
+* a corrupted byte is caught by the slice CRC;
+* the configuration record the product builds on the host
+  (pp_ffv1_encoder_create with no context) equals the oracle's byte for byte
+  and parses to the documented fields.
+"""
+import numpy as np
+import pytest
+
+import ffv1_ref as ref
+import pyoracle as po
+import synth
+from pixpath import ffv1
+
+FMTS = [("yuv422p10le", po.YUV422P10LE, 10, 1, 0), ("yuv420p", po.YUV420P, 8, 1, 1),
+        ("yuv420p10le", po.YUV420P10LE, 10, 1, 1), ("yuv422p", po.YUV422P, 8, 1, 0)]
+
+
+@pytest.mark.parametrize("name,fid,bits,hs,vs", FMTS, ids=[f[0] for f in FMTS])
+@pytest.mark.parametrize("kind", ["noise", "smooth", "checker", "steps"])
+@pytest.mark.parametrize("grid", [(1, 1), (2, 2), (4, 3)])
+def test_oracle_round_trip(name, fid, bits, hs, vs, kind, grid):
+    w, h = 192, 108
+    rng = np.random.default_rng(hash((name, kind, grid)) & 0xffff)
+    if kind == "noise":
+        planes = synth.noise_frame(rng, fid, w, h)
+    elif kind == "smooth":
+        planes = synth.smooth_frame(7, fid, w, h)
+    else:
+        planes = synth.extreme_frame(kind, fid, w, h, seams_x=(50, 100), seams_y=(30,))
+    extra = ref.extradata(bits, hs, vs, *grid)
+    pkt = ref.encode_frame(planes, bits, hs, vs, *grid)
+    rc, dec = ref.decode_frame(extra, pkt, w, h, bits, hs, vs)
+    assert rc == 0
+    for p in range(3):
+        np.testing.assert_array_equal(dec[p], planes[p])
+
+
+def test_slice_crc_catches_corruption():
+    planes = synth.noise_frame(np.random.default_rng(5), po.YUV422P10LE, 128, 64)
+    extra = ref.extradata(10, 1, 0, 2, 2)
+    pkt = bytearray(ref.encode_frame(planes, 10, 1, 0, 2, 2))
+    pkt[len(pkt) // 3] ^= 0x10
+    rc, _ = ref.decode_frame(extra, bytes(pkt), 128, 64, 10, 1, 0)
+    assert rc == -3
+
+
+@pytest.mark.parametrize("name,fid,bits,hs,vs", FMTS, ids=[f[0] for f in FMTS])
+@pytest.mark.parametrize("grid", [(1, 1), (4, 4), (8, 6)])
+def test_product_configuration_record(name, fid, bits, hs, vs, grid):
+    enc = ffv1.Ffv1Encoder(name, 1920, 1080, slices=grid, host_only=True)
+    x = enc.extradata
+    assert x == ref.extradata(bits, hs, vs, *grid)
+    rc, info = ref.parse_extradata(x)
+    assert rc == 0 and info["crc_ok"] == 1
+    assert (info["version"], info["micro_version"], info["coder_type"], info["ec"], info["intra"]) == (3, 4, 1, 1, 1)
+    assert (info["bits"], info["hsub"], info["vsub"]) == (bits, hs, vs)
+    assert (info["num_h_slices"], info["num_v_slices"], info["context_count"]) == (grid[0], grid[1], 666)
+    assert ref.crc(x) == 0

@@ -1,0 +1,78 @@
+"""FFV1 encoder on the GPU against the CPU
+restatement: every frame packet byte-identical to oracle/ffv1_oracle.c's,
+and decoded back to the input by the oracle's decoder (lossless; the slice
+CRCs and FFmpeg's end-of-slice position check pass).  Parity against FFmpeg
+itself is unpinned (no FFV1 implementation exists in this container or on
+the box)."""
+import numpy as np
+import pytest
+
+import ffv1_ref as ref
+import pyoracle as po
+import synth
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("yuv422p10le", po.YUV422P10LE, 10, 1, 0), ("yuv420p", po.YUV420P, 8, 1, 1),
+         ("yuv420p10le", po.YUV420P10LE, 10, 1, 1), ("yuv422p", po.YUV422P, 8, 1, 0)]
+
+
+def _batch(gpu, name, frames):
+    from pixpath.frames import FrameBatch
+    return FrameBatch.from_numpy(name, [np.stack([f[p] for f in frames]) for p in range(3)], device=gpu)
+
+
+@pytest.mark.parametrize("name,fid,bits,hs,vs", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("w,h,grid", [(640, 360, (4, 4)), (330, 190, (3, 2)), (1920, 1080, (4, 4))])
+def test_gpu_packets_match_oracle(gpu, name, fid, bits, hs, vs, w, h, grid):
+    from pixpath import ffv1
+    rng = np.random.default_rng(w + h)
+    frames = [synth.noise_frame(rng, fid, w, h), synth.smooth_frame(3, fid, w, h),
+              synth.extreme_frame("steps", fid, w, h, seams_x=(w // 3,), seams_y=(h // 2,))]
+    if w * h > 1_000_000:
+        frames = frames[1:2]  # the C oracle takes ~1 s per 1080p frame
+    enc = ffv1.Ffv1Encoder(name, w, h, slices=grid, max_frames=len(frames), device=gpu)
+    pkts = enc.encode_to_host(_batch(gpu, name, frames))
+    extra = enc.extradata
+    assert extra == ref.extradata(bits, hs, vs, *grid)
+    for f, planes in enumerate(frames):
+        want = ref.encode_frame(planes, bits, hs, vs, *grid)
+        if pkts[f] != want:
+            n = min(len(pkts[f]), len(want))
+            first = next((i for i in range(n) if pkts[f][i] != want[i]), n)
+            pytest.fail("frame %d: %d vs %d bytes, first difference at %d" % (f, len(pkts[f]), len(want), first))
+        rc, dec = ref.decode_frame(extra, pkts[f], w, h, bits, hs, vs)
+        assert rc == 0
+        for p in range(3):
+            np.testing.assert_array_equal(dec[p], planes[p])
+
+
+def test_gpu_600_frames_lossless(gpu):
+    """A config-2-sized AVPVS batch (600 distinct 1080p yuv422p10le frames) in
+    one encode: packet sizes add up, and the first, a middle and the last
+    frame decode back to their inputs."""
+    import torch
+    from pixpath import ffv1
+    from pixpath.frames import FrameBatch
+    n = 600
+    src = FrameBatch("yuv422p10le", 1920, 1080, n, device=gpu)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(600)
+    base = torch.arange(1920, device=gpu, dtype=torch.int32)
+    for p in range(3):
+        v = src.view(p)
+        ramp = (base[: v.shape[2]] * (p + 1)) % 880 + 64
+        noise = torch.randint(0, 8, v.shape, generator=g, device=gpu, dtype=torch.int32)
+        fr = torch.arange(n, device=gpu, dtype=torch.int32).view(n, 1, 1)
+        v.copy_(((ramp.view(1, 1, -1) + noise + fr) % 1024).to(v.dtype))
+    enc = ffv1.Ffv1Encoder("yuv422p10le", 1920, 1080, slices=(4, 4), max_frames=n, device=gpu)
+    buf, sizes = enc.encode(src)
+    assert buf.numel() == int(sizes.sum()) and (sizes > 0).all()
+    data = buf.cpu().numpy().tobytes()
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    extra = enc.extradata
+    for f in (0, 299, n - 1):
+        rc, dec = ref.decode_frame(extra, data[offs[f]:offs[f + 1]], 1920, 1080, 10, 1, 0)
+        assert rc == 0
+        for p in range(3):
+            np.testing.assert_array_equal(dec[p], src.view(p)[f].cpu().numpy())
