@@ -73,7 +73,8 @@ def parse():
     ap.add_argument("--pvs-per-rank", type=int, default=32)
     ap.add_argument("--pvs-total", type=int, default=None, help="fixed batch size (strong scaling), e.g. 256")
     ap.add_argument("--pool", type=int, default=8, help="distinct resident PVS inputs per rank")
-    ap.add_argument("--workload", default="config2", choices=sorted(list(WORKLOADS) + ["config4"]))
+    ap.add_argument("--workload", default="config2", choices=sorted(list(WORKLOADS) + ["config4", "ffv1"]))
+    ap.add_argument("--ffv1-slices", default="8x8", help="FFV1 slice grid (workload ffv1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="per CPU-baseline stage")
@@ -235,6 +236,8 @@ def main():
     torch.cuda.set_device(dev)
     if args.workload == "config4":
         return bench_stall(args, rank, world, dev)
+    if args.workload == "ffv1":
+        return bench_ffv1(args, rank, world, dev)
 
     from pixpath import ops
     from pixpath.frames import FrameBatch
@@ -420,6 +423,67 @@ def bench_stall(args, rank, world, dev):
                                        "traffic": None, "algorithmic_bytes_per_launch": 2 * fb * n,
                                        "avg_launch_ms": round(ms, 4)},
                           "canvas_chain": canvas, "cpu_baseline": None}), flush=True)
+    return 0
+
+
+def bench_ffv1(args, rank, world, dev):
+    """FFV1 encode of the config-2 AVPVS (600 frames of 1920x1080 yuv422p10le,
+    SURVEY.md section 8f row 1): frames/s through the GPU encoder (one lane per
+    slice, packets laid out in HBM), against the CPU restatement on a bounded
+    sample.  Content: smooth gradients moving per frame plus +-4 noise (a
+    compressible picture; pure noise is FFV1's worst case)."""
+    import time
+    import numpy as np
+    import torch
+    from pixpath import ffv1
+    from pixpath.frames import FrameBatch
+    w, h, n = 1920, 1080, args.frames
+    nh, nv = (int(v) for v in args.ffv1_slices.split("x"))
+    src = FrameBatch("yuv422p10le", w, h, n, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(910 + rank)
+    fr = torch.arange(n, device=dev, dtype=torch.int32).view(n, 1, 1)
+    for p in range(3):
+        v = src.view(p)
+        yy = torch.arange(v.shape[1], device=dev, dtype=torch.int32).view(1, -1, 1)
+        xx = torch.arange(v.shape[2], device=dev, dtype=torch.int32).view(1, 1, -1)
+        noise = torch.randint(-4, 5, v.shape, generator=g, device=dev, dtype=torch.int32)
+        v.copy_(((xx * (p + 1) + yy * 2 + 3 * fr) % 800 + 100 + noise).clamp(64, 940).to(v.dtype))
+    enc = ffv1.Ffv1Encoder("yuv422p10le", w, h, slices=(nh, nv), max_frames=n, device=dev)
+    for _ in range(args.warmup):
+        enc.encode(src)
+    torch.cuda.synchronize()
+    from pixpath import batch as batch_barrier
+    batch_barrier.barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        buf, sizes = enc.encode(src)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    dt = batch_barrier.max_over_ranks(dt, world)
+    raw = frame_bytes("yuv422p10le", w, h)
+    out = {"metric": "FFV1 AVPVS encode frames/s (1080p yuv422p10le)", "value": round(world * n / dt, 1),
+           "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "u16", "data": "synthetic (moving gradients + uniform noise in [-4, 4])",
+           "config": {"workload": "ffv1: FFV1 v3 intra encode of a 600-frame config-2 AVPVS", "frames": n,
+                      "slices": [nh, nv], "bytes_per_frame": round(float(sizes.mean()), 1),
+                      "compression": round(raw / float(sizes.mean()), 3)},
+           "roofline": None}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import ffv1_ref
+        k = 3
+        frames = [[src.view(p)[f].cpu().numpy() for p in range(3)] for f in range(k)]
+        t0 = time.perf_counter()
+        for f in frames:
+            ffv1_ref.encode_frame(f, 10, 1, 0, nh, nv)
+        cdt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(k / cdt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": "%d frames through oracle/ffv1_oracle.c (gcc -O3, one thread)" % k,
+                               "cpu_model": host_cpu()[0]}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
     return 0
 
 
