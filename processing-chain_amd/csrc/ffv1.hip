@@ -32,6 +32,7 @@ namespace pp {
 constexpr int kFfv1Ctx = 666;   // (11^3 + 1) / 2 contexts per plane set
 constexpr int kCtxSize = 32;    // state bytes per context
 constexpr int kStateBytes = 2 * kFfv1Ctx * kCtxSize + 64;  // + slice-header states, keyframe and end bits
+constexpr int kSlotStride = 40;  // LDS bytes per lane for the cached context
 
 // ---- host range coder (configuration record) and state tables -------------
 struct HostRC {
@@ -234,6 +235,11 @@ __device__ inline int ldpx(const uint8_t *row, int x) {
 __global__ __launch_bounds__(64) void ffv1_slice_kernel(const Ffv1Args a) {
     __shared__ uint8_t s_zero[256], s_one[256];
     __shared__ uint32_t s_crc[256];
+    // the 32 state bytes of the context the lane is coding with, cached in LDS
+    // (stride 40 B: 2-way bank conflicts at most); written back to HBM when the
+    // lane switches context, so put_symbol's ~10 dependent state accesses per
+    // sample are LDS round trips instead of L1/L2 ones
+    __shared__ __align__(16) uint8_t s_ctx[64 * kSlotStride];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
         s_zero[i] = a.tables[i];
         s_one[i] = a.tables[256 + i];
@@ -265,6 +271,24 @@ __global__ __launch_bounds__(64) void ffv1_slice_kernel(const Ffv1Args a) {
     const int x0 = (int)((int64_t)sx * a.w / a.nh), x1 = (int)((int64_t)(sx + 1) * a.w / a.nh);
     const int y0 = (int)((int64_t)sy * a.h / a.nv), y1 = (int)((int64_t)(sy + 1) * a.h / a.nv);
     const int mask = (1 << a.bits) - 1, half = 1 << (a.bits - 1);
+    uint8_t *const slot = s_ctx + threadIdx.x * kSlotStride;
+    int cur_key = -1;  // (plane set, context) held in `slot`
+    auto switch_ctx = [&](int key) {
+        if (cur_key >= 0) {
+            uint2 *g = reinterpret_cast<uint2 *>(st0 + cur_key * kCtxSize);
+            const uint2 *l = reinterpret_cast<const uint2 *>(slot);
+#pragma unroll
+            for (int i = 0; i < 4; i++) g[i] = l[i];
+        }
+        const uint2 *g = reinterpret_cast<const uint2 *>(st0 + key * kCtxSize);
+        uint2 *l = reinterpret_cast<uint2 *>(slot);
+        uint2 v[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) v[i] = g[i];
+#pragma unroll
+        for (int i = 0; i < 4; i++) l[i] = v[i];
+        cur_key = key;
+    };
     for (int p = 0; p < 3; p++) {
         const int pw = p ? ((x1 - x0) + (1 << a.hsub) - 1) >> a.hsub : x1 - x0;
         const int ph = p ? ((y1 - y0) + (1 << a.vsub) - 1) >> a.vsub : y1 - y0;
@@ -274,7 +298,7 @@ __global__ __launch_bounds__(64) void ffv1_slice_kernel(const Ffv1Args a) {
         const int64_t ls = p == 0 ? a.ls[0] : p == 1 ? a.ls[1] : a.ls[2];
         const int64_t fs = p == 0 ? a.fs[0] : p == 1 ? a.fs[1] : a.fs[2];
         const uint8_t *base = src + frame * fs + (int64_t)py0 * ls + (int64_t)px0 * a.bytes;
-        uint8_t *const st = st0 + (p ? kFfv1Ctx * kCtxSize : 0);
+        const int key0 = p ? kFfv1Ctx : 0;
         for (int y = 0; y < ph; y++) {
             const uint8_t *row = base + (int64_t)y * ls;
             const uint8_t *top = row - ls, *top2 = row - 2 * ls;
@@ -284,9 +308,19 @@ __global__ __launch_bounds__(64) void ffv1_slice_kernel(const Ffv1Args a) {
             int T = y > 0 ? (a.bytes == 2 ? ldpx<uint16_t>(top, 0) : ldpx<uint8_t>(top, 0)) : 0;
             int TL = y > 1 ? (a.bytes == 2 ? ldpx<uint16_t>(top2, 0) : ldpx<uint8_t>(top2, 0)) : 0;
             int L = T;
+            // samples one column ahead are loaded before the current one is
+            // coded, so their latency hides behind the range coder
+            auto ld = [&](const uint8_t *r, int x) {
+                return a.bytes == 2 ? ldpx<uint16_t>(r, x) : ldpx<uint8_t>(r, x);
+            };
+            int nv = ld(row, 0);
+            int ntr = pw > 1 ? (y > 0 ? ld(top, 1) : 0) : T;
             for (int x = 0; x < pw; x++) {
-                const int TR = x + 1 < pw ? (y > 0 ? (a.bytes == 2 ? ldpx<uint16_t>(top, x + 1) : ldpx<uint8_t>(top, x + 1)) : 0) : T;
-                const int v = a.bytes == 2 ? ldpx<uint16_t>(row, x) : ldpx<uint8_t>(row, x);
+                const int TR = ntr, v = nv;
+                if (x + 1 < pw) {
+                    nv = ld(row, x + 1);
+                    ntr = x + 2 < pw ? (y > 0 ? ld(top, x + 2) : 0) : TR;
+                }
                 int ctx = dquant((L - TL) & 0xFF) + 11 * dquant((TL - T) & 0xFF) + 121 * dquant((T - TR) & 0xFF);
                 int diff = v - median3(L, L + T - TL, T);
                 if (ctx < 0) {
@@ -295,7 +329,8 @@ __global__ __launch_bounds__(64) void ffv1_slice_kernel(const Ffv1Args a) {
                 }
                 diff &= mask;
                 diff = diff >= half ? diff - (mask + 1) : diff;
-                c.symbol(st + ctx * kCtxSize, diff, true);
+                if (key0 + ctx != cur_key) switch_ctx(key0 + ctx);
+                c.symbol(slot, diff, true);
                 TL = T;
                 T = TR;
                 L = v;
