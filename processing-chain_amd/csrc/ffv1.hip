@@ -313,14 +313,19 @@ __global__ __launch_bounds__(64) void ffv1_slice_kernel(const Ffv1Args a) {
             auto ld = [&](const uint8_t *r, int x) {
                 return a.bytes == 2 ? ldpx<uint16_t>(r, x) : ldpx<uint8_t>(r, x);
             };
+            // top row two columns ahead (tr1 = TR of the next column), so the
+            // next column's context -- and the HBM state block it needs, when
+            // it differs from the current one -- is known before this column
+            // is coded: the block's load overlaps the range coder
             int nv = ld(row, 0);
-            int ntr = pw > 1 ? (y > 0 ? ld(top, 1) : 0) : T;
+            int tr0 = pw > 1 ? (y > 0 ? ld(top, 1) : 0) : T;
+            int tr1 = pw > 2 ? (y > 0 ? ld(top, 2) : 0) : tr0;
+            int pre_key = -1;
+            uint2 pre[4];
             for (int x = 0; x < pw; x++) {
-                const int TR = ntr, v = nv;
-                if (x + 1 < pw) {
-                    nv = ld(row, x + 1);
-                    ntr = x + 2 < pw ? (y > 0 ? ld(top, x + 2) : 0) : TR;
-                }
+                const int TR = tr0, v = nv;
+                if (x + 1 < pw) nv = ld(row, x + 1);
+                const int tr2 = x + 3 < pw ? (y > 0 ? ld(top, x + 3) : 0) : tr1;
                 int ctx = dquant((L - TL) & 0xFF) + 11 * dquant((TL - T) & 0xFF) + 121 * dquant((T - TR) & 0xFF);
                 int diff = v - median3(L, L + T - TL, T);
                 if (ctx < 0) {
@@ -329,8 +334,34 @@ __global__ __launch_bounds__(64) void ffv1_slice_kernel(const Ffv1Args a) {
                 }
                 diff &= mask;
                 diff = diff >= half ? diff - (mask + 1) : diff;
-                if (key0 + ctx != cur_key) switch_ctx(key0 + ctx);
+                const int key = key0 + ctx;
+                if (key != cur_key) {
+                    if (key == pre_key) {  // prefetched: write the old block back, install the new
+                        uint2 *g = reinterpret_cast<uint2 *>(st0 + cur_key * kCtxSize);
+                        uint2 *l = reinterpret_cast<uint2 *>(slot);
+#pragma unroll
+                        for (int i = 0; i < 4; i++) g[i] = l[i];
+#pragma unroll
+                        for (int i = 0; i < 4; i++) l[i] = pre[i];
+                        cur_key = key;
+                    } else {
+                        switch_ctx(key);
+                    }
+                }
+                // next column: L = v, TL = T, T = TR, TR = tr1
+                if (x + 1 < pw) {
+                    int c1 = dquant((v - T) & 0xFF) + 11 * dquant((T - TR) & 0xFF) + 121 * dquant((TR - tr1) & 0xFF);
+                    const int k1 = key0 + (c1 < 0 ? -c1 : c1);
+                    if (k1 != key) {
+                        const uint2 *g = reinterpret_cast<const uint2 *>(st0 + k1 * kCtxSize);
+#pragma unroll
+                        for (int i = 0; i < 4; i++) pre[i] = g[i];
+                        pre_key = k1;
+                    }
+                }
                 c.symbol(slot, diff, true);
+                tr0 = tr1;
+                tr1 = tr2;
                 TL = T;
                 T = TR;
                 L = v;

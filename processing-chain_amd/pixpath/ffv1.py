@@ -19,7 +19,7 @@ from .ops import _stream, context
 
 
 class Ffv1Encoder:
-    def __init__(self, fmt, w, h, slices=(4, 4), max_frames=600, device=None, host_only=False):
+    def __init__(self, fmt, w, h, slices=(8, 8), max_frames=600, device=None, host_only=False):
         self.fmt = formats.fmt(fmt)
         self.w, self.h = int(w), int(h)
         self.slices = (int(slices[0]), int(slices[1]))
