@@ -1052,6 +1052,47 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
     return PP_OK;
 }
 
+// GENERIC_UYVY on the strip path: one strip_kernel<.., FUSE = 1> launch whose
+// planes store straight into the uyvy422 rows (U Y V Y byte order)
+int launch_packed(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, int nframes, hipStream_t st) {
+    using namespace pp;
+    ScaleArgs a{};
+    a.nplanes = 3;
+    static const int off[3] = {1, 0, 2}, step[3] = {2, 4, 4};
+    for (int p = 0; p < 3; ++p) {
+        a.pl[p] = P->fjob[p];
+        a.pl[p].pk_off = off[p];
+        a.pl[p].pk_step = step[p];
+        a.src[p] = static_cast<const uint8_t *>(src->data[p]);
+        a.sls[p] = src->linesize[p];
+        a.sfs[p] = src->frame_stride[p];
+        a.dst[p] = static_cast<uint8_t *>(dst->data[0]);
+        a.dls[p] = dst->linesize[0];
+        a.dfs[p] = dst->frame_stride[0];
+    }
+    a.hshift = P->si.depth == 8 ? 7 : P->si.depth - 1;
+    a.dither = 0;  // yuv2packedX rounds with 1 << 18, never dithers
+    a.vec_src = 1;
+    a.vec_dst = 0;
+    const int vtm = strip_vtm_bucket(std::max(P->fjob[0].vtp, P->fjob[1].vtp));
+    KernelFn k = P->si.depth == 8 ? pick_strip_packed_u8(P->fast_hw, vtm) : pick_strip_packed_u16(P->fast_hw, vtm);
+    if (!k) PP_FAIL(PP_ERR_UNSUPPORTED, "no packed kernel for window %d", P->fast_hw);
+    const int tiles = P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y;
+    a.tiles = tiles;
+    const int fmax = std::max(1, (1 << 30) / tiles);
+    for (int f0 = 0; f0 < nframes; f0 += fmax) {
+        const int nf = std::min(fmax, nframes - f0);
+        ScaleArgs b = a;
+        for (int p = 0; p < 3; ++p) {
+            b.src[p] += f0 * a.sfs[p];
+            b.dst[p] += f0 * a.dfs[p];
+        }
+        hipLaunchKernelGGL(k, dim3(tiles * nf), dim3(kThreads), P->fast_lds, st, b);
+    }
+    PP_HIP(hipGetLastError());
+    return PP_OK;
+}
+
 // CHAIN, fused: one strip_kernel<.., FUSE = target depth> launch
 int launch_chain(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, int nframes, hipStream_t st) {
     using namespace pp;
@@ -1149,6 +1190,9 @@ static int execute_kind(pp_scale_plan *P, pp_scale_plan::Kind kind, const pp_fra
         return pp_scale_execute(P->stage2, &tmp, dst, nframes, stream);
     }
     case pp_scale_plan::GENERIC_UYVY: {
+        bool vsrc = true;
+        for (int p = 0; p < 3; ++p) vsrc &= aligned(src->data[p], src->linesize[p], nframes > 1 ? src->frame_stride[p] : 0, 16);
+        if (P->fast_hw && vsrc) return launch_packed(P, src, dst, nframes, st);
         // yuv2packedX: planar 8-bit 4:2:2 (flat rounding) then interleave
         const int64_t yb = (int64_t)P->dw * P->dh, cb = (int64_t)P->cdw * P->cdh;
         const int64_t per = yb + 2 * cb;

@@ -66,6 +66,7 @@ struct PlaneJob {
     int vtp2;               // second-stage V tap pairs (fuse 2)
     const int32_t *vrow2;   // [dh2][16] second-stage row records (base row, tap pairs)
     const int32_t *chunk2;  // [nch][4] per chunk: second-stage rows [lo2, hi2), ring2 base row, kept pairs
+    int pk_off, pk_step;    // strip_kernel FUSE == 1: byte offset / step of this plane in the uyvy422 row
 };
 
 struct ScaleArgs {
@@ -209,6 +210,9 @@ KernelFn pick_strip_u8(int outb, int hw, int vtm);
 // chain plans: first stage to 8 bit, second stage into `out2` (8/10) bits
 KernelFn pick_strip_chain_u16(int out2, int hw, int vtm);
 KernelFn pick_strip_chain_u8(int out2, int hw, int vtm);
+// GENERIC_UYVY plans: 8-bit samples stored straight into the packed uyvy422 row
+KernelFn pick_strip_packed_u16(int hw, int vtm);
+KernelFn pick_strip_packed_u8(int hw, int vtm);
 int strip_vtm_bucket(int vtp);
 
 }  // namespace pp

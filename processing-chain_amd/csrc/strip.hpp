@@ -71,7 +71,11 @@ __device__ inline void store4(uint8_t *drow, int xo, const int o[4], bool vec, i
     }
 }
 
-// FUSE (chain plans, pp_scale_chain_plan_create; register bound for 3 waves per
+// FUSE == 1 (GENERIC_UYVY plans: scale straight into uyvy422, swscale's
+// yuv2packedX with its flat 1 << 18 rounding): every plane stores its 8-bit
+// samples into the one packed row, byte J.pk_off + x * J.pk_step (Y: 1, 2;
+// U: 0, 4; V: 2, 4) -- no planar scratch, no interleave pass.
+// FUSE >= 8 (chain plans, pp_scale_chain_plan_create; register bound for 3 waves per
 // SIMD -- ring2 puts the plan's LDS at ~3 workgroups per CU anyway): 0 = plain plan; 8 / 10 = the
 // two-stage chain of create_avpvs_segment -- this kernel's 8-bit (OUTB == 8)
 // output is the overlay's yuv420p, and the per-plane mode J.fuse applies
@@ -84,7 +88,7 @@ __device__ inline void store4(uint8_t *drow, int xo, const int o[4], bool vec, i
 //     each chunk the second stage's vertical filter (vrow2, chunk2 tables)
 //     emits every output row whose taps are all in the ring.
 template <typename ST, int OUTB, int HW, int VTM, int FUSE = 0>
-__global__ __launch_bounds__(kThreads, (FUSE ? 3 : strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
+__global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
     extern __shared__ __align__(16) uint16_t lds[];
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int frame = L / a.tiles;
@@ -225,7 +229,7 @@ __global__ __launch_bounds__(kThreads, (FUSE ? 3 : strip_min_waves<(int)sizeof(S
             moved = true;
         }
         int base2 = 0;
-        if constexpr (FUSE != 0) {
+        if constexpr (FUSE >= 8) {
             if (J.fuse == 2) {  // ring2 keeps the rows the pending second-stage outputs still read
                 base2 = chunk2[4 * ci + 2];
                 const int shift2 = ci ? (base2 - chunk2[4 * ci - 2]) >> 1 : 0, keep2 = chunk2[4 * ci + 3];
@@ -336,7 +340,7 @@ __global__ __launch_bounds__(kThreads, (FUSE ? 3 : strip_min_waves<(int)sizeof(S
                     int o[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) o[j] = min(max(acc[j] >> sh, 0), mx);
-                    if constexpr (FUSE != 0) {
+                    if constexpr (FUSE >= 8) {
                         if (J.fuse == 2) {  // into ring2 (second-stage input), 15-bit
                             uint16_t *r16 = reinterpret_cast<uint16_t *>(ring2 + ((y - base2) >> 1) * kTileW + cx);
 #pragma unroll
@@ -355,7 +359,12 @@ __global__ __launch_bounds__(kThreads, (FUSE ? 3 : strip_min_waves<(int)sizeof(S
                             continue;
                         }
                     }
-                    if constexpr (OUTB == 8) {
+                    if constexpr (FUSE == 1) {
+                        uint8_t *pk = drow_p + J.pk_off;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (xo + j < J.dw) pk[(xo + j) * J.pk_step] = (uint8_t)o[j];
+                    } else if constexpr (OUTB == 8) {
                         if (lane_full && a.vec_dst) {
                             *reinterpret_cast<uint32_t *>(drow_p + xo) =
                                 (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | ((uint32_t)o[3] << 24);
@@ -393,7 +402,7 @@ __global__ __launch_bounds__(kThreads, (FUSE ? 3 : strip_min_waves<(int)sizeof(S
         case 7: if constexpr (VTM >= 7) vpass(std::integral_constant<int, 7>{}); break;
         default: if constexpr (VTM >= 8) vpass(std::integral_constant<int, 8>{}); break;
         }
-        if constexpr (FUSE != 0) {
+        if constexpr (FUSE >= 8) {
             // ---- second stage (fuse 2): vertical filter of the ring2 rows ----
             if (J.fuse == 2) {
                 __syncthreads();  // this chunk's first-stage rows are in ring2

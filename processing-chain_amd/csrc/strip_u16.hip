@@ -19,4 +19,8 @@ KernelFn pick_strip_chain_u16(int out2, int hw, int vtm) {
     PP_STRIP_HW_F(uint16_t, 8, 10)
 }
 
+KernelFn pick_strip_packed_u16(int hw, int vtm) {
+    PP_STRIP_HW_F(uint16_t, 8, 1)
+}
+
 }  // namespace pp

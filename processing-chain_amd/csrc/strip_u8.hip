@@ -17,4 +17,8 @@ KernelFn pick_strip_chain_u8(int out2, int hw, int vtm) {
     PP_STRIP_HW_F(uint8_t, 8, 10)
 }
 
+KernelFn pick_strip_packed_u8(int hw, int vtm) {
+    PP_STRIP_HW_F(uint8_t, 8, 1)
+}
+
 }  // namespace pp

@@ -19,6 +19,7 @@ processes of the reference's ParallelRunner pool get N different GPUs).
 """
 import argparse
 import ast
+import hashlib
 import json
 import os
 import sys
@@ -111,6 +112,13 @@ def cmd_avpvs(args):
     cap = int(round(float(args.duration) * float(rate))) if args.duration else None
     inner = _open_writer(out, target, W, H, rate, args.vopts, args.aopts,
                          None if args.aopts.strip() == "-an" else args.input, args.y)
+    stall = None
+    if args.stall_output:
+        # create_avpvs_short of a PVS with stalls: compose the stalled AVPVS
+        # (the bufferer step's output) from the frames this pass writes
+        stall = _StallOutput(args.stall_output, target, W, H, rate, args.buffer, args.skipping, args.spinner,
+                             args.black_frame, args.stall_vopts, args.stall_aopts, args.input, True, dev)
+        inner = _Tee(inner, stall.push, fb)
     wr = CountingWriter(inner, fb, cap)
     emit = _fps_counts(rd.rate, rate) if args.fps else None
     Pipeline(stage, batch=args.batch, device=dev).run(rd, wr, emit=emit)
@@ -119,7 +127,29 @@ def cmd_avpvs(args):
             wr.write(wr.last)
     rd.close()
     wr.close()
+    if stall is not None:
+        import json
+        stall.close()
+        with open(_record_path(args.stall_output), "w") as f:
+            json.dump(_stall_record(out, args.buffer, args.skipping, args.spinner, args.black_frame, args.pix_fmt,
+                                    args.stall_vopts, args.stall_aopts), f)
     return 0
+
+
+class _Tee:
+    """Writer that also pushes each written frame into a StallStream pusher."""
+
+    def __init__(self, inner, push, frame_bytes):
+        self.inner, self.push, self.fb = inner, push, frame_bytes
+
+    def write(self, frames):
+        self.inner.write(frames)
+        mv = np.frombuffer(memoryview(frames).cast("B"), np.uint8)
+        for i in range(len(mv) // self.fb):
+            self.push.push(mv[i * self.fb:(i + 1) * self.fb].copy())
+
+    def close(self):
+        self.inner.close()
 
 
 def cmd_encseg(args):
@@ -231,69 +261,128 @@ def cmd_cpvs(args):
 from .stall import stall_schedule  # noqa: E402,F401  (PP-STALL-1, re-exported for callers/tests)
 
 
+class _StallOutput:
+    """The PP-STALL-1 output side (p03_generateAvPvs.py:236-243): a writer
+    plus a frame-by-frame StallStream pusher.  Input frames pass through;
+    stall runs are composed on the GPU from the retained frame (frozen frame or
+    black + spinner) and the audio gets the stalls' silence.  Shared by
+    `cli stall` (reading the AVPVS) and `cli avpvs --stall-output` (fed by
+    the AVPVS writer itself, no second decode)."""
+
+    def __init__(self, out, fmt, w, h, rate, buffer, skipping, spinner_path, black_frame, vopts, aopts,
+                 audio_input, overwrite, dev):
+        import torch
+        from . import io as pio, ops, spinner
+        from .frames import FrameBatch
+        from .stall import StallStream, stall_audio_graph, stall_times
+        device = torch.device("cuda", dev)
+        events = ast.literal_eval(buffer)
+        delays = None
+        if not skipping:
+            anim, delays = spinner.load_apng(spinner_path)
+            ops.spinner_upload(anim, fmt, device=dev)
+        audio_from, graph = None, None
+        if aopts.strip() != "-an" and os.path.splitext(out)[1].lower() not in (".y4m", ".raw", ".yuv"):
+            ap = pio.audio_params(audio_input)  # pragma: no cover - needs ffprobe
+            if ap is not None:
+                audio_from = audio_input
+                if not skipping:
+                    graph = stall_audio_graph(stall_times(events, rate), ap[0], ap[1])
+        if audio_from:  # pragma: no cover - needs ffmpeg
+            self.wr = pio.FFmpegWriter(out, fmt, w, h, rate, vopts, aopts, audio_from=audio_from,
+                                       overwrite="-y" if overwrite else "-n", audio_filter=graph)
+        else:
+            self.wr = _open_writer(out, fmt, w, h, rate, vopts, aopts, None, overwrite)
+        self.fb = fb = formats_frame_bytes(fmt, w, h)
+        self.fmt, self.w, self.h, self.device = fmt, w, h, device
+        self.src_b = FrameBatch.interleaved(fmt, w, h, 1, device=device)
+        self.blk = 256
+        self.dst_b = FrameBatch.interleaved(fmt, w, h, self.blk, device=device)
+        self.host = torch.empty((self.blk, fb), dtype=torch.uint8).pin_memory()
+        self.push = StallStream(events, rate, skipping, delays, black_frame=black_frame).pusher(
+            self.wr.write, self._emit_stall)
+
+    def _emit_stall(self, f, spin):
+        import torch
+        from . import ops
+        from .frames import FrameBatch
+        fmt, w, h, fb, device = self.fmt, self.w, self.h, self.fb, self.device
+        if f is not None:
+            self.src_b.storage.copy_(torch.from_numpy(np.asarray(f)).view(1, fb).to(device, non_blocking=False))
+        for i in range(0, len(spin), self.blk):
+            part = spin[i:i + self.blk]
+            n = len(part)
+            ops.stall_compose(self.src_b, [0 if f is not None else -1] * n, part,
+                              dst=FrameBatch.interleaved(fmt, w, h, n, device=device,
+                                                         storage=self.dst_b.storage[:n]))
+            self.host[:n].copy_(self.dst_b.storage[:n])  # synchronous D2H into pinned memory
+            self.wr.write(self.host[:n].numpy())
+
+    def close(self):
+        n = self.push.close()
+        self.wr.close()
+        return n
+
+
+def formats_frame_bytes(fmt, w, h):
+    from . import formats
+    return formats.frame_bytes(fmt, w, h)
+
+
+# Provenance of a stalled AVPVS written by `cli avpvs --stall-output`: the
+# bufferer step (`cli stall`) keeps that output when this record matches its
+# own arguments and the AVPVS it would read is the one the record names.
+def _stall_record(input_path, buffer, skipping, spinner_path, black_frame, pix_fmt, vopts, aopts):
+    st = os.stat(input_path)
+    spin = None
+    if not skipping:
+        with open(spinner_path, "rb") as f:
+            spin = hashlib.sha256(f.read()).hexdigest()
+    return {"input": os.path.abspath(input_path), "input_size": st.st_size, "input_mtime_ns": st.st_mtime_ns,
+            "buffer": buffer, "skipping": bool(skipping), "spinner_sha256": spin, "black_frame": bool(black_frame),
+            "pix_fmt": pix_fmt, "vopts": vopts, "aopts": aopts}
+
+
+def _record_path(out):
+    return out + ".pixpath-stall.json"
+
+
 def cmd_stall(args):
     """bufferer replacement (p03_generateAvPvs.py:236-243, spec PP-STALL-1):
     the AVPVS is read once, in order; input frames pass through untouched,
     stall runs are composed on the GPU from the one retained frame (frozen
-    frame or black + spinner), and the audio gets the stalls' silence."""
+    frame or black + spinner), and the audio gets the stalls' silence.
+    An output the AVPVS pass already composed (`cli avpvs --stall-output`,
+    same arguments, same AVPVS) is kept as is: no second decode/encode."""
+    import json
     import torch
-    from . import io as pio, ops, spinner
-    from .frames import FrameBatch
-    from .stall import StallStream, stall_audio_graph, stall_times
+    from . import io as pio
     out = args.output
-    if _skip(out, args.y):
+    rec = _record_path(out)
+    if os.path.isfile(rec) and os.path.isfile(out):
+        try:
+            want = _stall_record(args.input, args.buffer, args.skipping, args.spinner, args.black_frame,
+                                 args.pix_fmt, args.vopts, args.aopts)
+            have = json.load(open(rec))
+        except (OSError, ValueError):
+            want, have = None, {}
+        if want == have:
+            print("pixpath: %s was composed with the AVPVS pass; kept" % out, file=sys.stderr)
+            return 0
+        os.remove(out)  # a speculative output for other arguments: ours to replace
+        os.remove(rec)
+    elif _skip(out, args.y):
         return 0
     dev = _device()
     torch.cuda.set_device(dev)
-    device = torch.device("cuda", dev)
     rd = pio.open_reader(args.input)
-    fmt, w, h = rd.fmt, rd.w, rd.h
-    events = ast.literal_eval(args.buffer)
-    delays = None
-    if not args.skipping:
-        anim, delays = spinner.load_apng(args.spinner)
-        ops.spinner_upload(anim, fmt, device=dev)
-    audio_from, graph = None, None
-    if args.aopts.strip() != "-an" and os.path.splitext(out)[1].lower() not in (".y4m", ".raw", ".yuv"):
-        ap = pio.audio_params(args.input)  # pragma: no cover - needs ffprobe
-        if ap is not None:
-            audio_from = args.input
-            if not args.skipping:
-                graph = stall_audio_graph(stall_times(events, rd.rate), ap[0], ap[1])
-    if audio_from:  # pragma: no cover - needs ffmpeg
-        wr = pio.FFmpegWriter(out, fmt, w, h, rd.rate, args.vopts, args.aopts, audio_from=audio_from,
-                              overwrite="-y" if args.y else "-n", audio_filter=graph)
-    else:
-        wr = _open_writer(out, fmt, w, h, rd.rate, args.vopts, args.aopts, None, args.y)
-    fb = rd.frame_bytes
-    src_b = FrameBatch.interleaved(fmt, w, h, 1, device=device)
-    blk = 256
-    dst_b = FrameBatch.interleaved(fmt, w, h, blk, device=device)
-    host = torch.empty((blk, fb), dtype=torch.uint8).pin_memory()
-
-    def frames():
-        buf = np.empty((1, fb), np.uint8)
-        while rd.read_into(buf, 1) == 1:
-            yield buf[0].copy()
-
-    def emit_input(f):
-        wr.write(f)
-
-    def emit_stall(f, spin):
-        if f is not None:
-            src_b.storage.copy_(torch.from_numpy(f).view(1, fb).to(device, non_blocking=False))
-        for i in range(0, len(spin), blk):
-            part = spin[i:i + blk]
-            n = len(part)
-            ops.stall_compose(src_b, [0 if f is not None else -1] * n, part,
-                              dst=FrameBatch.interleaved(fmt, w, h, n, device=device, storage=dst_b.storage[:n]))
-            host[:n].copy_(dst_b.storage[:n])  # synchronous D2H into pinned memory
-            wr.write(host[:n].numpy())
-
-    StallStream(events, rd.rate, args.skipping, delays, black_frame=args.black_frame).run(
-        frames(), emit_input, emit_stall)
+    so = _StallOutput(out, rd.fmt, rd.w, rd.h, rd.rate, args.buffer, args.skipping, args.spinner, args.black_frame,
+                      args.vopts, args.aopts, args.input, args.y, dev)
+    buf = np.empty((1, rd.frame_bytes), np.uint8)
+    while rd.read_into(buf, 1) == 1:
+        so.push.push(buf[0].copy())
     rd.close()
-    wr.close()
+    so.close()
     return 0
 
 
@@ -339,6 +428,14 @@ def main(argv=None):
     p.add_argument("--fps", default=None)
     p.add_argument("--duration", default=None)
     p.add_argument("--overlay-yuv420", action="store_true")
+    # the stalled AVPVS in the same pass (p03's bufferer step, fused)
+    p.add_argument("--stall-output", default=None)
+    p.add_argument("--buffer", default="[]")
+    p.add_argument("--spinner", default=None)
+    p.add_argument("--skipping", action="store_true")
+    p.add_argument("--black-frame", action="store_true")
+    p.add_argument("--stall-vopts", default="-c:v ffv1")
+    p.add_argument("--stall-aopts", default="-c:a pcm_s16le")
     p.set_defaults(fn=cmd_avpvs)
 
     p = sub.add_parser("encseg")

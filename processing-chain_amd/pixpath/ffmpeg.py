@@ -226,6 +226,14 @@ def create_avpvs_short(pvs, overwrite=False, scale_avpvs_tosource=False, force_6
             # to ffmpeg, which rejects it and the run fails (lib/ffmpeg.py:958-961);
             # the GPU backend hands over the same literal and fails the same way
             args += ["--fps", "{src_framerate}"]
+        spinner = default_spinner_path()
+        if pvs.has_buffering() and (pvs.has_framefreeze() or spinner):
+            # p03's bufferer step composed in this same pass (section 8f-3):
+            # `cli stall` later keeps the output when its arguments match
+            # (bufferer_command with p03's default --spinner-path)
+            args += ["--stall-output", pvs.get_avpvs_file_path(),
+                     "--buffer", buffer_string(pvs.get_buff_events_media_time()), "--black-frame"]
+            args += ["--skipping"] if pvs.has_framefreeze() else ["--spinner", spinner]
         return _collapse(_gpu_cli("avpvs", args + [output_file]))
 
     cmd = """
@@ -420,6 +428,21 @@ def audio_mux(pvs, overwrite=False):
     -c:v copy -ac 2 -c:a pcm_s16le -map 0:v -map 1:a
     {output_file}""".format(**locals())
     return _collapse(cmd)
+
+
+def default_spinner_path():
+    """p03's default --spinner-path (lib/parse_args.py:97-100:
+    <reference>/util/spinner-128-white.png), from PIXPATH_SPINNER or the
+    imported reference package; None when neither is known."""
+    env = os.environ.get("PIXPATH_SPINNER")
+    if env:
+        return env
+    mod = sys.modules.get("lib.parse_args") or sys.modules.get("lib.ffmpeg")
+    if mod is not None and getattr(mod, "__file__", None):
+        p = os.path.abspath(os.path.join(os.path.dirname(mod.__file__), "..", "util", "spinner-128-white.png"))
+        if os.path.isfile(p):
+            return p
+    return None
 
 
 def bufferer_command(pvs, spinner_path, force=False):

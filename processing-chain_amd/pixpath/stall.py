@@ -95,38 +95,62 @@ class StallStream:
             self.stalls = [(int(round(t * self.rate)), int(round(d * self.rate))) for t, d in ev]
 
     def run(self, frames, emit_input, emit_stall):
-        if self.skipping:
-            return self._run_freeze(frames, emit_input)
-        last, i, k = None, 0, 0
+        p = self.pusher(emit_input, emit_stall)
         for f in frames:
-            while k < len(self.stalls) and self.stalls[k][0] <= i:
-                # a stall at t=0: black (--black-frame) or the first frame itself
-                src = last if i > 0 else (None if self.black_frame else f)
-                emit_stall(src, spinner_indices(self.stalls[k][1], self.rate, self.delays))
-                k += 1
-            emit_input(f)
-            last, i = f, i + 1
-        while k < len(self.stalls):  # stalls at or past the end show the last frame
-            src = last if i > 0 else None
-            emit_stall(src, spinner_indices(self.stalls[k][1], self.rate, self.delays))
-            k += 1
-        return i
+            p.push(f)
+        return p.close()
 
-    def _run_freeze(self, frames, emit_input):
-        prev, i = None, 0
-        held = {}  # span start a -> its frozen frame (the ORIGINAL frame a-1, or frame 0)
-        for f in frames:
-            # the last span (in sorted order) covering i decides, as in stall_schedule
-            owner = None
-            for a, b in self.spans:
-                if a <= i < b:
-                    owner = a
-            for a, _ in self.spans:
-                if a == i and a not in held:
-                    held[a] = prev if a > 0 else f
-            emit_input(f if owner is None else held[owner])
-            prev, i = f, i + 1
-        return i
+    def pusher(self, emit_input, emit_stall):
+        """The same walk, frame by frame: ``push(frame)`` for every input frame
+        in order, then ``close()`` (returns the input frame count).  Lets the
+        AVPVS writer compose the stalled output while it writes the AVPVS."""
+        return _FreezePush(self, emit_input) if self.skipping else _StallPush(self, emit_input, emit_stall)
+
+
+class _StallPush:
+    def __init__(self, s, emit_input, emit_stall):
+        self.s, self.emit_input, self.emit_stall = s, emit_input, emit_stall
+        self.last, self.i, self.k = None, 0, 0
+
+    def push(self, f):
+        s = self.s
+        while self.k < len(s.stalls) and s.stalls[self.k][0] <= self.i:
+            # a stall at t=0: black (--black-frame) or the first frame itself
+            src = self.last if self.i > 0 else (None if s.black_frame else f)
+            self.emit_stall(src, spinner_indices(s.stalls[self.k][1], s.rate, s.delays))
+            self.k += 1
+        self.emit_input(f)
+        self.last, self.i = f, self.i + 1
+
+    def close(self):
+        s = self.s
+        while self.k < len(s.stalls):  # stalls at or past the end show the last frame
+            src = self.last if self.i > 0 else None
+            self.emit_stall(src, spinner_indices(s.stalls[self.k][1], s.rate, s.delays))
+            self.k += 1
+        return self.i
+
+
+class _FreezePush:
+    def __init__(self, s, emit_input):
+        self.s, self.emit_input = s, emit_input
+        self.prev, self.i = None, 0
+        self.held = {}  # span start a -> its frozen frame (the ORIGINAL frame a-1, or frame 0)
+
+    def push(self, f):
+        # the last span (in sorted order) covering i decides, as in stall_schedule
+        owner = None
+        for a, b in self.s.spans:
+            if a <= self.i < b:
+                owner = a
+        for a, _ in self.s.spans:
+            if a == self.i and a not in self.held:
+                self.held[a] = self.prev if a > 0 else f
+        self.emit_input(f if owner is None else self.held[owner])
+        self.prev, self.i = f, self.i + 1
+
+    def close(self):
+        return self.i
 
 
 def stall_audio_graph(stalls, sample_rate, channel_layout):

@@ -69,3 +69,27 @@ def test_freeze_with_skipping_keeps_length():
     assert len(seq) == 50
     assert seq[10:15] == [(9, -1)] * 5 and seq[15] == (15, -1)
     assert seq[30:32] == [(29, -1)] * 2
+
+
+def test_gpu_avpvs_short_composes_stalls_in_the_same_pass(monkeypatch):
+    """gpu backend: create_avpvs_short of a PVS with stalls also writes the
+    stalled AVPVS (--stall-output), with the bufferer step's own arguments."""
+    import types
+    from pixpath import ffmpeg as pff
+    monkeypatch.setenv("PIXPATH_SPINNER", "/opt/spinner.png")
+    monkeypatch.setattr(pff, "_backend", "gpu")
+    pp = types.SimpleNamespace(coding_width=1920, coding_height=1080)
+    ql = types.SimpleNamespace(width=1280, height=720)
+    seg = types.SimpleNamespace(quality_level=ql, get_segment_file_path=lambda: "/db/seg0.mkv")
+    pvs = types.SimpleNamespace(
+        test_config=types.SimpleNamespace(post_processings=[pp]), has_buffering=lambda: True,
+        has_framefreeze=lambda: False, get_avpvs_wo_buffer_file_path=lambda: "/db/avpvs/P_wo.avi",
+        get_avpvs_file_path=lambda: "/db/avpvs/P.avi", segments=[seg], get_pix_fmt_for_avpvs=lambda: "yuv422p10le",
+        src=types.SimpleNamespace(stream_info={"coded_width": 3840, "coded_height": 2160}),
+        get_buff_events_media_time=lambda: [[4, 1.5], [8, 1.0]])
+    cmd = pff.create_avpvs_short(pvs, overwrite=True)
+    assert "--stall-output /db/avpvs/P.avi --buffer '[[4,1.5],[8,1.0]]' --black-frame --spinner /opt/spinner.png" in cmd
+    assert cmd.endswith("/db/avpvs/P_wo.avi")
+    monkeypatch.delenv("PIXPATH_SPINNER")
+    monkeypatch.setattr(pff, "default_spinner_path", lambda: None)
+    assert "--stall-output" not in pff.create_avpvs_short(pvs, overwrite=True)

@@ -176,3 +176,36 @@ def test_cli_encseg_trim_scale_select_fps(gpu, tmp_path, in_fps, out_fps, n, sta
         ref = po.scale(po.YUV422P10LE, frames[skip + k], po.YUV420P, 256, h, po.SWS_BICUBIC)
         for p in range(3):
             np.testing.assert_array_equal(got[p][j], ref[p], err_msg="out %d <- in %d plane %d" % (j, skip + k, p))
+
+
+@pytest.mark.parametrize("mode", ["spinner", "skipping"])
+def test_cli_avpvs_with_fused_stall(gpu, tmp_path, mode):
+    """Section 8f-3: create_avpvs_short of a PVS with stalls composes the
+    stalled AVPVS in the same pass (`cli avpvs --stall-output`).  Its output
+    equals what the bufferer step (`cli stall`) makes from the written AVPVS;
+    that step then keeps it (no second decode); with other arguments it
+    regenerates."""
+    import os
+    from pixpath import cli
+    rng = np.random.default_rng(8)
+    frames = [synth.noise_frame(rng, po.YUV420P10LE, 320, 180) for _ in range(40)]
+    src = str(tmp_path / "seg.y4m")
+    _write_y4m(src, "yuv420p10le", frames, 320, 180, rate=60)
+    wo, fused, plain = (str(tmp_path / n) for n in ("wo_buffer.y4m", "pvs.y4m", "plain.y4m"))
+    buf = "[[0.1,0.1],[0.5,0.05]]" if mode == "spinner" else "[[0.1,0.1],[0.3,0.05]]"
+    extra = ["--spinner", GOLDEN_SPINNER] if mode == "spinner" else ["--skipping"]
+    assert cli.main(["avpvs", "-y", "--input", src, "--size", "640x360", "--pix-fmt", "yuv422p10le",
+                     "--batch", "16", "--stall-output", fused, "--buffer", buf, "--black-frame"] + extra + [wo]) == 0
+    assert os.path.isfile(fused + ".pixpath-stall.json")
+    stall_args = ["--input", wo, "--buffer", buf, "--pix-fmt", "yuv422p10le", "--black-frame", "--vopts", "-c:v ffv1",
+                  "--aopts", "-c:a pcm_s16le"] + extra
+    assert cli.main(["stall", "-y"] + stall_args + [plain]) == 0
+    assert open(fused, "rb").read() == open(plain, "rb").read()
+    before = os.stat(fused).st_mtime_ns
+    assert cli.main(["stall", "-y"] + stall_args + [fused]) == 0  # kept
+    assert os.stat(fused).st_mtime_ns == before
+    other = stall_args[:]
+    other[other.index(buf)] = "[[0.2,0.1]]"
+    assert cli.main(["stall", "-n"] + other + [fused]) == 0       # speculative output replaced
+    assert cli.main(["stall", "-y"] + other + [plain]) == 0
+    assert open(fused, "rb").read() == open(plain, "rb").read()

@@ -33,6 +33,9 @@ CASES = [
     (po.YUV422P, 1920, 1080, po.UYVY422, 1920, 1080, po.SWS_BICUBIC, "noise"),          # a5 interleave
     (po.YUV420P, 1920, 1080, po.UYVY422, 1920, 1080, po.SWS_BICUBIC, "noise"),          # a5 generic packed
     (po.YUV420P10LE, 640, 360, po.UYVY422, 640, 360, po.SWS_BICUBIC, "noise"),
+    (po.YUV420P, 1280, 720, po.UYVY422, 1920, 1080, po.SWS_BICUBIC, "noise"),          # scale into uyvy422: one launch
+    (po.YUV422P10LE, 1280, 720, po.UYVY422, 1920, 1080, po.SWS_LANCZOS, "smooth"),
+    (po.YUV420P, 333, 197, po.UYVY422, 500, 300, po.SWS_BICUBIC, "noise"),             # ragged strips, packed
     (po.YUV420P, 3840, 2160, po.YUV420P, 640, 360, po.SWS_BICUBIC, "smooth"),          # 6x downscale (narrow strips)
     (po.YUV422P10LE, 3840, 2160, po.YUV422P10LE, 960, 540, po.SWS_LANCZOS, "noise"),   # 4x lanczos (24+ taps)
     (po.YUV420P, 640, 360, po.YUV420P, 3840, 2160, po.SWS_BICUBIC, "noise"),           # 6x upscale
