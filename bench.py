@@ -462,6 +462,18 @@ def bench_ffv1(args, rank, world, dev):
     dt = (time.perf_counter() - t0) / args.steps
     dt = batch_barrier.max_over_ranks(dt, world)
     raw = frame_bytes("yuv422p10le", w, h)
+    # decode of the same packets (host packets -> H2D -> one lane per slice)
+    pk = buf.cpu().numpy().tobytes()
+    dec = ffv1.Ffv1Decoder(enc.extradata, w, h, max_frames=n, device=dev)
+    back = FrameBatch("yuv422p10le", w, h, n, device=dev)
+    dec.decode(pk, sizes, dst=back)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dec.decode(pk, sizes, dst=back)
+    torch.cuda.synchronize()
+    ddt = batch_barrier.max_over_ranks((time.perf_counter() - t0) / args.steps, world)
+    lossless = all(bool(torch.equal(back.view(p), src.view(p))) for p in range(3))
     out = {"metric": "FFV1 AVPVS encode frames/s (1080p yuv422p10le)", "value": round(world * n / dt, 1),
            "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -469,6 +481,8 @@ def bench_ffv1(args, rank, world, dev):
            "config": {"workload": "ffv1: FFV1 v3 intra encode of a 600-frame config-2 AVPVS", "frames": n,
                       "slices": [nh, nv], "bytes_per_frame": round(float(sizes.mean()), 1),
                       "compression": round(raw / float(sizes.mean()), 3)},
+           "decode": {"frames_per_s": round(world * n / ddt, 1), "ms_per_step": round(ddt * 1e3, 3),
+                      "lossless": lossless, "note": "packets from host memory (H2D included)"},
            "roofline": None}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

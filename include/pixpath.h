@@ -254,6 +254,22 @@ int pp_ffv1_encoder_destroy(pp_ffv1_enc *enc);
 int pp_ffv1_extradata(const pp_ffv1_enc *enc, uint8_t *out, int cap);
 int64_t pp_ffv1_encode(pp_ffv1_enc *enc, const pp_frames *src, int nframes, uint8_t *dst,
                        int64_t dst_cap, int64_t *frame_sizes, void *stream);
+/* FFV1 decoder (the CPVS stage reads the AVPVS back, lib/ffmpeg.py:1149):
+ * version 3 intra streams with the range coder's default state table, one
+ * quantisation table set of up to 3 inputs, <= 256 slices, 8/10-bit
+ * 4:2:0/4:2:2 -- what pp_ffv1_encode writes.  pp_ffv1_decoder_create parses
+ * and checks the configuration record (ctx == NULL: record check only);
+ * pp_ffv1_decoder_format gives the PP_FMT_* of the decoded frames;
+ * pp_ffv1_decode decodes nframes packets held back to back in HOST memory
+ * (frame_sizes[f] bytes each) into dst (device), checking every slice's CRC,
+ * header and end position; synchronises `stream`. */
+typedef struct pp_ffv1_dec pp_ffv1_dec;
+int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extradata, int extradata_size, int w, int h,
+                           int max_frames, pp_ffv1_dec **out);
+int pp_ffv1_decoder_destroy(pp_ffv1_dec *dec);
+int pp_ffv1_decoder_format(const pp_ffv1_dec *dec);
+int pp_ffv1_decode(pp_ffv1_dec *dec, const uint8_t *packets, const int64_t *frame_sizes, int nframes,
+                   const pp_frames *dst, void *stream);
 
 #ifdef __cplusplus
 }

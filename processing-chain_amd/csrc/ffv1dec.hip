@@ -1,0 +1,421 @@
+// FFV1 version 3 decoder on gfx950 (the decode
+// half): reads AVPVS frame packets back into planar frames in HBM for the
+// CPVS stage (create_cpvs decodes the FFV1 AVPVS, lib/ffmpeg.py:1149-1201).
+//
+// Same shape as the encoder (ffv1.hip): ONE LANE PER SLICE over every slice of
+// every frame of the batch.  The host walks each packet's slice footers
+// backwards (24-bit sizes, RFC 9043 4.8) into a slice table; a lane checks
+// its slice's CRC-32 parity, reads the keyframe bit (first slice), the slice
+// header (position from the header, as FFmpeg's decode_slice_header), then
+// decodes Y, Cb, Cr in raster order -- quantised context from the record's
+// tables (LDS), median prediction, get_symbol through the slice's own context
+// states (current context cached in LDS, as in the encoder) -- writing each
+// sample straight into the destination planes, whose previous row it reads
+// back for T / TL / TR.  It finishes with the closing bit at state 129 and
+// FFmpeg's end-of-slice position check.  Per-slice status: 0 ok, 1 CRC,
+// 2 header, 3 end mismatch.
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "common.hpp"
+#include "device.hpp"
+
+namespace pp {
+
+void rac_states(uint8_t zero[256], uint8_t one[256]);  // ffv1.hip
+void crc_table(uint32_t t[256]);
+
+namespace {
+
+constexpr int kCtx = 32;
+constexpr int kMaxCtx = 4096;              // context count the state blocks are sized for
+constexpr int kSlot = 40;
+
+struct HostRD {
+    int low = 0, range = 0xFF00;
+    const uint8_t *p = nullptr, *end = nullptr;
+    uint8_t zero[256], one[256];
+    HostRD(const uint8_t *b, int64_t n) {
+        rac_states(zero, one);
+        p = b;
+        end = b + n;
+        low = n >= 2 ? (b[0] << 8) | b[1] : 0;
+        p += 2;
+        if (low >= 0xFF00) { low = 0xFF00; end = p; }
+    }
+    void refill() {
+        if (range < 0x100) {
+            range <<= 8;
+            low <<= 8;
+            if (p < end) low += *p++;
+        }
+    }
+    int rac(uint8_t *st) {
+        const int r1 = (range * *st) >> 8;
+        range -= r1;
+        if (low < range) {
+            *st = zero[*st];
+            refill();
+            return 0;
+        }
+        low -= range;
+        *st = one[*st];
+        range = r1;
+        refill();
+        return 1;
+    }
+    int symbol(uint8_t *st) {  // unsigned
+        if (rac(st)) return 0;
+        int e = 0;
+        while (rac(st + 1 + std::min(e, 9))) {
+            if (++e > 31) return -1;
+        }
+        int a = 1;
+        for (int i = e - 1; i >= 0; i--) a += a + rac(st + 22 + std::min(i, 9));
+        return a;
+    }
+};
+
+}  // namespace
+
+struct Ffv1DecArgs {
+    const uint8_t *pkt;
+    const int64_t *soff, *slen;  // [nslices] slice start and length (trailer included)
+    uint8_t *dst[3];
+    int64_t ls[3], fs[3];
+    int w, h, bytes, bits, hsub, vsub, nh, nv, nslices, ec;
+    int ctx_count;               // contexts per plane set (record's tables)
+    int64_t state_bytes;         // per slice: 2 * ctx_count * 32 + 64
+    uint8_t *states;             // [nslices][state_bytes], primed to 128
+    int *status;
+    const uint8_t *tables;       // zero[256], one[256], crc table
+    const int16_t *quant;        // [3][256] (scaled)
+};
+
+struct DevRD {
+    int low, range;
+    const uint8_t *p, *end;
+    const uint8_t *zero, *one;
+    __device__ __forceinline__ void refill() {
+        if (range < 0x100) {
+            range <<= 8;
+            low <<= 8;
+            if (p < end) low += *p++;
+        }
+    }
+    __device__ __forceinline__ int rac(uint8_t *st) {
+        const int sv = *st;
+        const int r1 = (range * sv) >> 8;
+        range -= r1;
+        if (low < range) {
+            *st = zero[sv];
+            refill();
+            return 0;
+        }
+        low -= range;
+        *st = one[sv];
+        range = r1;
+        refill();
+        return 1;
+    }
+    __device__ __forceinline__ int symbol(uint8_t *st, bool is_signed) {
+        if (rac(st)) return 0;
+        int e = 0;
+        while (rac(st + 1 + min(e, 9))) {
+            if (++e > 31) return 0;
+        }
+        int a = 1;
+        for (int i = e - 1; i >= 0; i--) a += a + rac(st + 22 + min(i, 9));
+        return (is_signed && rac(st + 11 + min(e, 10))) ? -a : a;
+    }
+};
+
+__device__ __forceinline__ int dmedian3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
+
+__global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
+    __shared__ uint8_t s_zero[256], s_one[256];
+    __shared__ uint32_t s_crc[256];
+    __shared__ int16_t s_q[3][256];
+    __shared__ __align__(16) uint8_t s_ctx[64 * kSlot];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        s_zero[i] = a.tables[i];
+        s_one[i] = a.tables[256 + i];
+        s_crc[i] = reinterpret_cast<const uint32_t *>(a.tables + 512)[i];
+        s_q[0][i] = a.quant[i];
+        s_q[1][i] = a.quant[256 + i];
+        s_q[2][i] = a.quant[512 + i];
+    }
+    __syncthreads();
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= a.nslices) return;
+    const int per = a.nh * a.nv;
+    const int frame = g / per, s = g - frame * per;
+    const uint8_t *const sb = a.pkt + a.soff[g];
+    const int64_t n = a.slen[g];
+    if (a.ec) {  // CRC-32 parity of the whole slice, trailer included, must leave 0
+        uint32_t crc = 0;
+        for (int64_t i = 0; i < n; i++) crc = (crc << 8) ^ s_crc[(crc >> 24) ^ sb[i]];
+        if (crc) {
+            a.status[g] = 1;
+            return;
+        }
+    }
+    uint8_t *const st0 = a.states + (int64_t)g * a.state_bytes;
+    uint8_t *const hs = st0 + 2 * (int64_t)a.ctx_count * kCtx;
+    DevRD d;
+    d.zero = s_zero; d.one = s_one;
+    d.p = sb; d.end = sb + n; d.range = 0xFF00;
+    d.low = n >= 2 ? (sb[0] << 8) | sb[1] : 0;
+    d.p += 2;
+    if (d.low >= 0xFF00) { d.low = 0xFF00; d.end = d.p; }
+    if (s == 0 && !d.rac(hs + 32)) {  // keyframe bit
+        a.status[g] = 2;
+        return;
+    }
+    const int sx = d.symbol(hs, false), sy = d.symbol(hs, false);
+    const int sw = d.symbol(hs, false) + 1, sh = d.symbol(hs, false) + 1;
+    const int q0 = d.symbol(hs, false), q1 = d.symbol(hs, false), ps = d.symbol(hs, false);
+    d.symbol(hs, false);
+    d.symbol(hs, false);  // sample aspect ratio
+    if (sx < 0 || sy < 0 || sx > a.nh - sw || sy > a.nv - sh || q0 || q1 || ps != 3) {
+        a.status[g] = 2;
+        return;
+    }
+    const int x0 = (int)((int64_t)sx * a.w / a.nh), x1 = (int)((int64_t)(sx + sw) * a.w / a.nh);
+    const int y0 = (int)((int64_t)sy * a.h / a.nv), y1 = (int)((int64_t)(sy + sh) * a.h / a.nv);
+    const int mask = (1 << a.bits) - 1;
+    uint8_t *const slot = s_ctx + threadIdx.x * kSlot;
+    int cur_key = -1;
+    auto use_ctx = [&](int key) {
+        if (key == cur_key) return;
+        if (cur_key >= 0) {
+            uint2 *gp = reinterpret_cast<uint2 *>(st0 + cur_key * kCtx);
+            const uint2 *l = reinterpret_cast<const uint2 *>(slot);
+#pragma unroll
+            for (int i = 0; i < 4; i++) gp[i] = l[i];
+        }
+        const uint2 *gp = reinterpret_cast<const uint2 *>(st0 + key * kCtx);
+        uint2 *l = reinterpret_cast<uint2 *>(slot);
+        uint2 v[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) v[i] = gp[i];
+#pragma unroll
+        for (int i = 0; i < 4; i++) l[i] = v[i];
+        cur_key = key;
+    };
+    for (int p = 0; p < 3; p++) {
+        const int pw = p ? ((x1 - x0) + (1 << a.hsub) - 1) >> a.hsub : x1 - x0;
+        const int ph = p ? ((y1 - y0) + (1 << a.vsub) - 1) >> a.vsub : y1 - y0;
+        const int px0 = p ? x0 >> a.hsub : x0, py0 = p ? y0 >> a.vsub : y0;
+        uint8_t *dp = p == 0 ? a.dst[0] : p == 1 ? a.dst[1] : a.dst[2];
+        const int64_t ls = p == 0 ? a.ls[0] : p == 1 ? a.ls[1] : a.ls[2];
+        const int64_t fs = p == 0 ? a.fs[0] : p == 1 ? a.fs[1] : a.fs[2];
+        uint8_t *base = dp + frame * fs + (int64_t)py0 * ls + (int64_t)px0 * a.bytes;
+        const int key0 = p ? a.ctx_count : 0;
+        auto ld = [&](const uint8_t *r, int x) {
+            return a.bytes == 2 ? (int)reinterpret_cast<const uint16_t *>(r)[x] : (int)r[x];
+        };
+        for (int y = 0; y < ph; y++) {
+            uint8_t *row = base + (int64_t)y * ls;
+            const uint8_t *top = row - ls, *top2 = row - 2 * ls;
+            int T = y > 0 ? ld(top, 0) : 0;
+            int TL = y > 1 ? ld(top2, 0) : 0;
+            int L = T;
+            for (int x = 0; x < pw; x++) {
+                const int TR = x + 1 < pw ? (y > 0 ? ld(top, x + 1) : 0) : T;
+                int ctx = s_q[0][(L - TL) & 0xFF] + s_q[1][(TL - T) & 0xFF] + s_q[2][(T - TR) & 0xFF];
+                const bool neg = ctx < 0;
+                if (neg) ctx = -ctx;
+                use_ctx(key0 + ctx);
+                int diff = d.symbol(slot, true);
+                if (neg) diff = -diff;
+                const int v = (dmedian3(L, L + T - TL, T) + diff) & mask;
+                if (a.bytes == 2)
+                    reinterpret_cast<uint16_t *>(row)[x] = (uint16_t)v;
+                else
+                    row[x] = (uint8_t)v;
+                TL = T;
+                T = TR;
+                L = v;
+            }
+        }
+    }
+    hs[33] = 129;
+    d.rac(hs + 33);
+    a.status[g] = ((d.end - d.p) - 2 - 5 * (a.ec != 0)) != 0 ? 3 : 0;
+}
+
+}  // namespace pp
+
+using namespace pp;
+
+struct pp_ffv1_dec {
+    pp_ctx *ctx = nullptr;
+    int w = 0, h = 0, bits = 8, hsub = 1, vsub = 1, nh = 1, nv = 1, ec = 0, max_frames = 0, ctx_count = 0;
+    int16_t quant[3][256];
+    uint8_t *pkt = nullptr, *states = nullptr, *tables = nullptr;
+    int64_t pkt_cap = 0, *soff = nullptr, *slen = nullptr;
+    int *status = nullptr;
+    int16_t *dquant = nullptr;
+};
+
+extern "C" int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extra, int extra_size, int w, int h,
+                                      int max_frames, pp_ffv1_dec **out) {
+    if (!out || !extra) PP_FAIL(PP_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (w < 2 || h < 2 || max_frames < 1) PP_FAIL(PP_ERR_INVALID, "bad size %dx%d / max_frames %d", w, h, max_frames);
+    if (extra_size < 8) PP_FAIL(PP_ERR_INVALID, "configuration record of %d bytes", extra_size);
+    {
+        uint32_t t[256];
+        crc_table(t);
+        uint32_t crc = 0;
+        for (int i = 0; i < extra_size; i++) crc = (crc << 8) ^ t[(crc >> 24) ^ extra[i]];
+        if (crc) PP_FAIL(PP_ERR_INVALID, "configuration record CRC mismatch");
+    }
+    std::unique_ptr<pp_ffv1_dec> D(new pp_ffv1_dec());
+    D->ctx = ctx; D->w = w; D->h = h; D->max_frames = max_frames;
+    HostRD r(extra, extra_size);
+    uint8_t st[kCtx];
+    std::memset(st, 128, sizeof(st));
+    const int version = r.symbol(st);
+    const int micro = r.symbol(st);
+    const int coder = r.symbol(st);
+    const int cs = r.symbol(st);
+    D->bits = r.symbol(st);
+    const int chroma = r.rac(st);
+    D->hsub = r.symbol(st);
+    D->vsub = r.symbol(st);
+    const int alpha = r.rac(st);
+    D->nh = r.symbol(st) + 1;
+    D->nv = r.symbol(st) + 1;
+    const int tables = r.symbol(st);
+    (void)micro;
+    if (version != 3 || coder != 1 || cs != 0 || !chroma || alpha || tables != 1)
+        PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 record: version %d coder %d colorspace %d chroma %d alpha %d tables %d "
+                "(supported: 3, 1, 0, 1, 0, 1)", version, coder, cs, chroma, alpha, tables);
+    if ((D->bits != 8 && D->bits != 10) || D->hsub != 1 || D->vsub > 1)
+        PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 record: %d bits, chroma shifts %d/%d", D->bits, D->hsub, D->vsub);
+    if (D->nh < 1 || D->nv < 1 || D->nh * D->nv > 256 || D->nh > w || D->nv > h)
+        PP_FAIL(PP_ERR_INVALID, "FFV1 record: slice grid %dx%d", D->nh, D->nv);
+    // read_quant_tables: 5 run-length tables; only the first three may vary
+    int cc = 1;
+    for (int t = 0; t < 5; t++) {
+        uint8_t qs[kCtx];
+        std::memset(qs, 128, sizeof(qs));
+        int16_t q[256];
+        int i = 0, v = 0;
+        for (; i < 128; v++) {
+            const int len = r.symbol(qs) + 1;
+            if (len <= 0 || len > 128 - i) PP_FAIL(PP_ERR_INVALID, "FFV1 record: quantisation table %d", t);
+            for (int k = 0; k < len; k++) q[i++] = (int16_t)(cc * v);
+        }
+        for (i = 1; i < 128; i++) q[256 - i] = (int16_t)-q[i];
+        q[128] = (int16_t)-q[127];
+        const int levels = 2 * v - 1;
+        if (t >= 3 && levels != 1) PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 record: 5-input context model");
+        if (t < 3) std::memcpy(D->quant[t], q, sizeof(q));
+        cc *= levels;
+    }
+    D->ctx_count = (cc + 1) / 2;
+    if (D->ctx_count > kMaxCtx) PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 record: %d contexts", D->ctx_count);
+    if (r.rac(st)) PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 record: initial states");
+    D->ec = r.symbol(st);
+    const int intra = r.symbol(st);
+    if (intra != 1) PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 record: inter frames (intra %d)", intra);
+    if (!ctx) {
+        *out = D.release();
+        return PP_OK;
+    }
+    const int64_t ns = (int64_t)D->nh * D->nv * max_frames;
+    PP_HIP(hipSetDevice(ctx->device));
+    PP_HIP(hipMalloc(&D->states, (size_t)(2 * (int64_t)D->ctx_count * kCtx + 64) * ns));
+    PP_HIP(hipMalloc(&D->soff, sizeof(int64_t) * ns));
+    PP_HIP(hipMalloc(&D->slen, sizeof(int64_t) * ns));
+    PP_HIP(hipMalloc(&D->status, sizeof(int) * ns));
+    PP_HIP(hipMalloc(&D->tables, 512 + 1024));
+    PP_HIP(hipMalloc(&D->dquant, sizeof(D->quant)));
+    uint8_t tab[512 + 1024];
+    rac_states(tab, tab + 256);
+    crc_table(reinterpret_cast<uint32_t *>(tab + 512));
+    PP_HIP(hipMemcpy(D->tables, tab, sizeof(tab), hipMemcpyHostToDevice));
+    PP_HIP(hipMemcpy(D->dquant, D->quant, sizeof(D->quant), hipMemcpyHostToDevice));
+    *out = D.release();
+    return PP_OK;
+}
+
+extern "C" int pp_ffv1_decoder_destroy(pp_ffv1_dec *D) {
+    if (!D) return PP_OK;
+    for (void *p : {(void *)D->pkt, (void *)D->states, (void *)D->soff, (void *)D->slen, (void *)D->status,
+                    (void *)D->tables, (void *)D->dquant})
+        if (p) (void)hipFree(p);
+    delete D;
+    return PP_OK;
+}
+
+// Format of the decoded frames (PP_FMT_*), from the configuration record.
+extern "C" int pp_ffv1_decoder_format(const pp_ffv1_dec *D) {
+    if (!D) PP_FAIL(PP_ERR_INVALID, "null decoder");
+    if (D->bits == 8) return D->vsub ? PP_FMT_YUV420P : PP_FMT_YUV422P;
+    return D->vsub ? PP_FMT_YUV420P10LE : PP_FMT_YUV422P10LE;
+}
+
+extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int64_t *frame_sizes, int nframes,
+                              const pp_frames *dst, void *stream) {
+    if (!D || !packets || !frame_sizes || !dst || nframes < 0) PP_FAIL(PP_ERR_INVALID, "null argument");
+    if (!D->ctx) PP_FAIL(PP_ERR_INVALID, "host-only decoder cannot decode");
+    if (nframes > D->max_frames) PP_FAIL(PP_ERR_INVALID, "%d frames > max_frames %d", nframes, D->max_frames);
+    if (nframes == 0) return PP_OK;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    PP_HIP(hipSetDevice(D->ctx->device));
+    const int per = D->nh * D->nv, ns = per * nframes;
+    const int trailer = 3 + 5 * (D->ec != 0);
+    std::vector<int64_t> soff(ns), slen(ns);
+    int64_t base = 0;
+    for (int f = 0; f < nframes; ++f) {  // slices from the end of the packet (ffv1dec.c decode_frame)
+        int64_t end = base + frame_sizes[f];
+        for (int i = per - 1; i >= 0; --i) {
+            if (end - base < trailer) PP_FAIL(PP_ERR_INVALID, "frame %d: slice %d trailer missing", f, i);
+            const uint8_t *t = packets + end - trailer;
+            const int64_t v = ((int64_t)t[0] << 16 | t[1] << 8 | t[2]) + trailer;
+            if (i == 0 ? v != end - base : v > end - base)
+                PP_FAIL(PP_ERR_INVALID, "frame %d: slice pointer chain broken at slice %d", f, i);
+            end -= v;
+            soff[f * per + i] = end;
+            slen[f * per + i] = v;
+        }
+        base += frame_sizes[f];
+    }
+    if (base > D->pkt_cap) {
+        if (D->pkt) PP_HIP(hipFree(D->pkt));
+        D->pkt = nullptr;
+        D->pkt_cap = 0;
+        PP_HIP(hipMalloc(&D->pkt, base));
+        D->pkt_cap = base;
+    }
+    PP_HIP(hipMemcpyAsync(D->pkt, packets, base, hipMemcpyHostToDevice, st));
+    PP_HIP(hipMemcpyAsync(D->soff, soff.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
+    PP_HIP(hipMemcpyAsync(D->slen, slen.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
+    const int64_t sb = 2 * (int64_t)D->ctx_count * kCtx + 64;
+    PP_HIP(hipMemsetAsync(D->states, 128, (size_t)sb * ns, st));
+    Ffv1DecArgs a{};
+    a.pkt = D->pkt; a.soff = D->soff; a.slen = D->slen;
+    for (int p = 0; p < 3; ++p) {
+        a.dst[p] = static_cast<uint8_t *>(dst->data[p]);
+        a.ls[p] = dst->linesize[p];
+        a.fs[p] = dst->frame_stride[p];
+    }
+    a.w = D->w; a.h = D->h; a.bytes = D->bits > 8 ? 2 : 1; a.bits = D->bits; a.hsub = D->hsub; a.vsub = D->vsub;
+    a.nh = D->nh; a.nv = D->nv; a.nslices = ns; a.ec = D->ec;
+    a.ctx_count = D->ctx_count; a.state_bytes = sb;
+    a.states = D->states; a.status = D->status; a.tables = D->tables; a.quant = D->dquant;
+    hipLaunchKernelGGL(ffv1_decode_kernel, dim3((ns + 63) / 64), dim3(64), 0, st, a);
+    PP_HIP(hipGetLastError());
+    std::vector<int> status(ns);
+    PP_HIP(hipMemcpyAsync(status.data(), D->status, sizeof(int) * ns, hipMemcpyDeviceToHost, st));
+    PP_HIP(hipStreamSynchronize(st));
+    static const char *what[] = {"ok", "slice CRC mismatch", "bad slice header", "bytestream end mismatch"};
+    for (int i = 0; i < ns; ++i)
+        if (status[i]) PP_FAIL(PP_ERR_INVALID, "frame %d slice %d: %s", i / per, i % per, what[std::min(status[i], 3)]);
+    return PP_OK;
+}

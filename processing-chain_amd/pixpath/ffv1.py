@@ -72,3 +72,41 @@ class Ffv1Encoder:
             out.append(data[off:off + n])
             off += n
         return out
+
+
+class Ffv1Decoder:
+    """FFV1 v3 intra decoder on the GPU (one lane per slice): the AVPVS read
+    back for the CPVS stage.  ``decode(packets, sizes)`` takes the frame
+    packets back to back in host memory and returns a FrameBatch in HBM."""
+
+    def __init__(self, extradata, w, h, max_frames=600, device=None, host_only=False):
+        self.w, self.h, self.max_frames = int(w), int(h), int(max_frames)
+        self.ctx = None if host_only else context(device)
+        buf = (ctypes.c_uint8 * len(extradata)).from_buffer_copy(extradata)
+        h_ = ctypes.c_void_p()
+        check(lib().pp_ffv1_decoder_create(None if host_only else self.ctx.handle, buf, len(extradata), self.w,
+                                           self.h, self.max_frames, ctypes.byref(h_)))
+        self.handle = h_
+        fid = check(lib().pp_ffv1_decoder_format(h_))
+        self.fmt = formats.fmt(fid)
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            try:
+                lib().pp_ffv1_decoder_destroy(self.handle)
+            except Exception:
+                pass
+            self.handle = None
+
+    def decode(self, packets, sizes, dst=None, stream=None):
+        from .frames import FrameBatch
+        data = np.frombuffer(bytes(packets) if not isinstance(packets, (bytes, bytearray)) else packets, np.uint8)
+        sizes = np.ascontiguousarray(sizes, dtype=np.int64)
+        n = len(sizes)
+        if dst is None:
+            dst = FrameBatch(self.fmt, self.w, self.h, n, device=torch.device("cuda", self.ctx.device))
+        s = dst.frames_struct()
+        check(lib().pp_ffv1_decode(self.handle, data.ctypes.data_as(ctypes.c_void_p),
+                                   sizes.ctypes.data_as(ctypes.c_void_p), n, ctypes.byref(s),
+                                   _stream(dst.planes[0], stream)))
+        return dst

@@ -63,3 +63,16 @@ def test_product_configuration_record(name, fid, bits, hs, vs, grid):
     assert (info["bits"], info["hsub"], info["vsub"]) == (bits, hs, vs)
     assert (info["num_h_slices"], info["num_v_slices"], info["context_count"]) == (grid[0], grid[1], 666)
     assert ref.crc(x) == 0
+
+
+@pytest.mark.parametrize("name,fid,bits,hs,vs", FMTS, ids=[f[0] for f in FMTS])
+def test_product_decoder_reads_the_record(name, fid, bits, hs, vs):
+    """pp_ffv1_decoder_create (host-only) accepts the oracle's record, reports
+    the frame format, and refuses a record whose CRC parity is broken."""
+    x = ref.extradata(bits, hs, vs, 8, 8)
+    dec = ffv1.Ffv1Decoder(x, 1920, 1080, host_only=True)
+    assert dec.fmt.name == name
+    bad = bytearray(x)
+    bad[3] ^= 0x04
+    with pytest.raises(Exception, match="CRC"):
+        ffv1.Ffv1Decoder(bytes(bad), 1920, 1080, host_only=True)

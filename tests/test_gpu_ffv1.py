@@ -76,3 +76,58 @@ def test_gpu_600_frames_lossless(gpu):
         assert rc == 0
         for p in range(3):
             np.testing.assert_array_equal(dec[p], src.view(p)[f].cpu().numpy())
+
+
+@pytest.mark.parametrize("name,fid,bits,hs,vs", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("w,h,grid", [(640, 360, (4, 4)), (330, 190, (3, 2)), (1920, 1080, (8, 8))])
+def test_gpu_decoder_round_trip(gpu, name, fid, bits, hs, vs, w, h, grid):
+    """GPU encode -> GPU decode returns the input frames; the GPU decoder
+    also reads the C restatement's packets (the same bytes)."""
+    from pixpath import ffv1
+    rng = np.random.default_rng(w * 7 + h)
+    frames = [synth.noise_frame(rng, fid, w, h), synth.smooth_frame(5, fid, w, h),
+              synth.extreme_frame("checker", fid, w, h)]
+    enc = ffv1.Ffv1Encoder(name, w, h, slices=grid, max_frames=len(frames), device=gpu)
+    pkts = enc.encode_to_host(_batch(gpu, name, frames))
+    dec = ffv1.Ffv1Decoder(enc.extradata, w, h, max_frames=len(frames), device=gpu)
+    out = dec.decode(b"".join(pkts), [len(p) for p in pkts]).to_numpy()
+    for f, planes in enumerate(frames):
+        for p in range(3):
+            np.testing.assert_array_equal(out[p][f], planes[p])
+    if w * h < 1_000_000:
+        ref_pkt = ref.encode_frame(frames[0], bits, hs, vs, *grid)
+        out0 = dec.decode(ref_pkt, [len(ref_pkt)]).to_numpy()
+        for p in range(3):
+            np.testing.assert_array_equal(out0[p][0], frames[0][p])
+
+
+def test_gpu_decoder_rejects_corruption(gpu):
+    from pixpath import ffv1
+    rng = np.random.default_rng(3)
+    frames = [synth.noise_frame(rng, po.YUV422P10LE, 320, 180)]
+    enc = ffv1.Ffv1Encoder("yuv422p10le", 320, 180, slices=(2, 2), max_frames=1, device=gpu)
+    pkt = bytearray(enc.encode_to_host(_batch(gpu, "yuv422p10le", frames))[0])
+    dec = ffv1.Ffv1Decoder(enc.extradata, 320, 180, max_frames=1, device=gpu)
+    pkt[len(pkt) // 2] ^= 0x20
+    with pytest.raises(Exception, match="CRC|chain"):
+        dec.decode(bytes(pkt), [len(pkt)])
+
+
+def test_gpu_decode_600_frames(gpu):
+    """A whole 600-frame 1080p yuv422p10le AVPVS: GPU encode -> GPU decode, every frame equal."""
+    import torch
+    from pixpath import ffv1
+    from pixpath.frames import FrameBatch
+    n = 600
+    src = FrameBatch("yuv422p10le", 1920, 1080, n, device=gpu)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(60)
+    for p in range(3):
+        v = src.view(p)
+        v.copy_((torch.randint(0, 1024, v.shape, generator=g, device=gpu, dtype=torch.int32) // 16 * 16).to(v.dtype))
+    enc = ffv1.Ffv1Encoder("yuv422p10le", 1920, 1080, slices=(8, 8), max_frames=n, device=gpu)
+    buf, sizes = enc.encode(src)
+    dec = ffv1.Ffv1Decoder(enc.extradata, 1920, 1080, max_frames=n, device=gpu)
+    out = dec.decode(buf.cpu().numpy().tobytes(), sizes)
+    for p in range(3):
+        assert torch.equal(out.view(p)[:n], src.view(p)[:n])
