@@ -1,0 +1,156 @@
+"""AVI (with the OpenDML 2.0 extension) for one video stream of compressed
+frame packets -- the container of the reference's AVPVS (`<pvs>.avi`,
+lib/ffmpeg.py:951-954, FFV1 video) when the FFV1 encode runs on the GPU.
+
+Layout written (RIFF chunks, little-endian):
+  RIFF 'AVI ' [ LIST 'hdrl' [ avih, LIST 'strl' [ strh, strf (BITMAPINFOHEADER
+  + codec private data), indx (OpenDML super index) ], LIST 'odml' [ dmlh ] ],
+  LIST 'movi' [ '00dc' packets..., ix00 (standard index) ], idx1 ]
+  RIFF 'AVIX' [ LIST 'movi' [ '00dc'..., ix00 ] ] ...   (every RIFF < 1 GiB)
+The reader walks the chunks (it needs no index).  Round trips are tested
+here; acceptance by FFmpeg's avidec is unpinned (no FFmpeg in this
+environment).
+"""
+import struct
+from fractions import Fraction
+
+RIFF_LIMIT = 1 << 30  # bytes per RIFF (OpenDML readers expect < 1 GiB before AVIX)
+SUPER_ENTRIES = 256   # indx slots reserved (one per RIFF)
+
+
+def _chunk(fourcc, payload):
+    b = fourcc + struct.pack("<I", len(payload)) + payload
+    return b + (b"\0" if len(payload) & 1 else b"")
+
+
+class AviWriter:
+    def __init__(self, path, w, h, rate, extradata=b"", fourcc=b"FFV1", riff_limit=RIFF_LIMIT):
+        self.fh = open(path, "wb")
+        self.w, self.h, self.rate = int(w), int(h), Fraction(rate)
+        self.extradata, self.fourcc, self.limit = bytes(extradata), fourcc, riff_limit
+        self.riffs = []       # per RIFF: [riff_start, movi_start, [(data_offset, size, key)]]
+        self.total = 0
+        self.max_size = 0
+        self._write_headers()
+        self._open_movi()
+
+    # -- headers (patched on close) ------------------------------------------
+    def _write_headers(self):
+        self.fh.write(b"RIFF\0\0\0\0AVI ")
+        us = int(round(1e6 / float(self.rate)))
+        avih = struct.pack("<10I4I", us, 0, 0, 0x10 | 0x100, 0, 0, 1, 0, self.w, self.h, 0, 0, 0, 0)
+        num, den = self.rate.numerator, self.rate.denominator
+        strh = b"vids" + self.fourcc + struct.pack("<IHHIIIIIIiI4h", 0, 0, 0, 0, den, num, 0, 0, 0, -1, 0,
+                                                    0, 0, self.w, self.h)
+        bih = struct.pack("<IiiHH4sIiiII", 40 + len(self.extradata), self.w, self.h, 1, 24, self.fourcc,
+                          self.w * self.h * 3, 0, 0, 0, 0)
+        strf = bih + self.extradata
+        indx = struct.pack("<HBBI4s3I", 4, 0, 0, 0, b"00dc", 0, 0, 0) + b"\0" * (16 * SUPER_ENTRIES)
+        strl = b"strl" + _chunk(b"strh", strh) + _chunk(b"strf", strf) + _chunk(b"indx", indx)
+        odml = b"odml" + _chunk(b"dmlh", b"\0" * 248)
+        hdrl = b"hdrl" + _chunk(b"avih", avih) + _chunk(b"LIST", strl) + _chunk(b"LIST", odml)
+        self.hdr_start = self.fh.tell()
+        self.fh.write(_chunk(b"LIST", hdrl))
+        # offsets of the fields patched on close
+        base = self.hdr_start + 12
+        self.off_avih = base + 8                               # avih payload
+        strl_start = base + 8 + len(avih) + 8 + 4              # strl list payload after 'strl'
+        self.off_strh = strl_start + 8                         # strh payload
+        self.off_indx = strl_start + 8 + len(strh) + 8 + len(strf) + (len(strf) & 1) + 8
+        odml_start = self.off_indx + len(indx) + 8 + 4
+        self.off_dmlh = odml_start + 8
+
+    def _open_movi(self):
+        if self.riffs:
+            start = self.fh.tell()
+            self.fh.write(b"RIFF\0\0\0\0AVIX")
+        else:
+            start = 0
+        movi = self.fh.tell()
+        self.fh.write(b"LIST\0\0\0\0movi")
+        self.riffs.append([start, movi, []])
+
+    def _close_movi(self):
+        start, movi, ents = self.riffs[-1]
+        # ix00: standard index of this RIFF's packets, offsets relative to qwBaseOffset
+        ix = struct.pack("<HBBI4sQI", 2, 0, 1, len(ents), b"00dc", movi, 0)
+        ix += b"".join(struct.pack("<II", off - movi, size | (0 if key else 0x80000000)) for off, size, key in ents)
+        ix_pos = self.fh.tell()
+        self.fh.write(_chunk(b"ix00", ix))
+        end = self.fh.tell()
+        self._patch(movi + 4, end - movi - 8)
+        self.riffs[-1].append((ix_pos, len(ix) + 8))
+        if start == 0:  # idx1 (legacy index, first RIFF only): offsets relative to 'movi'
+            idx1 = b"".join(struct.pack("<4sIII", b"00dc", 0x10 if key else 0, off - 8 - (movi + 8), size)
+                            for off, size, key in ents)
+            self.fh.write(_chunk(b"idx1", idx1))
+            end = self.fh.tell()
+        self._patch(start + 4, end - start - 8)
+
+    def _patch(self, pos, value, fmt="<I"):
+        cur = self.fh.tell()
+        self.fh.seek(pos)
+        self.fh.write(struct.pack(fmt, value))
+        self.fh.seek(cur)
+
+    def write_packet(self, data, key=True):
+        data = bytes(data)
+        start = self.riffs[-1][0]
+        if self.fh.tell() - start + len(data) + 8 + 16 * (len(self.riffs[-1][2]) + 2) > self.limit \
+                and self.riffs[-1][2]:
+            self._close_movi()
+            self._open_movi()
+        off = self.fh.tell() + 8
+        self.fh.write(_chunk(b"00dc", data))
+        self.riffs[-1][2].append((off, len(data), key))
+        self.total += 1
+        self.max_size = max(self.max_size, len(data))
+
+    def close(self):
+        self._close_movi()
+        first = len(self.riffs[0][2])
+        # avih: dwMaxBytesPerSec, dwTotalFrames (first RIFF), dwSuggestedBufferSize
+        self._patch(self.off_avih + 4, int(self.max_size * float(self.rate)))
+        self._patch(self.off_avih + 16, first)
+        self._patch(self.off_avih + 28, self.max_size)
+        # strh: dwLength, dwSuggestedBufferSize
+        self._patch(self.off_strh + 32, self.total)
+        self._patch(self.off_strh + 36, self.max_size)
+        self._patch(self.off_dmlh, self.total)
+        # indx: one entry per RIFF's ix00
+        if len(self.riffs) > SUPER_ENTRIES:
+            raise ValueError("more than %d RIFF segments" % SUPER_ENTRIES)
+        self._patch(self.off_indx + 4, len(self.riffs))
+        for i, (_, _, ents, (ix_pos, ix_size)) in enumerate(self.riffs):
+            cur = self.fh.tell()
+            self.fh.seek(self.off_indx + 24 + 16 * i)
+            self.fh.write(struct.pack("<QII", ix_pos, ix_size, len(ents)))
+            self.fh.seek(cur)
+        self.fh.close()
+
+
+def read_packets(path):
+    """(info, packets): info = {w, h, rate, fourcc, extradata}; packets in order."""
+    info, packets = {}, []
+    with open(path, "rb") as fh:
+        data = fh.read()
+
+    def walk(pos, end):
+        while pos + 8 <= end:
+            tag, size = data[pos:pos + 4], struct.unpack_from("<I", data, pos + 4)[0]
+            body = pos + 8
+            if tag in (b"RIFF", b"LIST"):
+                walk(body + 4, body + size)
+            elif tag == b"strh":
+                scale, rate = struct.unpack_from("<II", data, body + 20)
+                info["rate"] = Fraction(rate, scale)
+                info["handler"] = data[body + 4:body + 8]
+            elif tag == b"strf":
+                bi_size, w, h = struct.unpack_from("<Iii", data, body)
+                info.update(w=w, h=abs(h), fourcc=data[body + 16:body + 20], extradata=data[body + 40:body + bi_size])
+            elif tag[2:] in (b"dc", b"db") and tag[:2].isdigit():
+                packets.append(data[body:body + size])
+            pos = body + size + (size & 1)
+
+    walk(0, len(data))
+    return info, packets

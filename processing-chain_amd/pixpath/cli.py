@@ -96,7 +96,11 @@ def cmd_avpvs(args):
         return 0
     dev = _device()
     torch.cuda.set_device(dev)
-    rd = pio.open_reader(args.input)
+    if args.ffv1_input:  # an AVPVS written by `--gpu-ffv1` (mobile CPVS scale reads it)
+        from .ffv1 import Ffv1AviReader
+        rd = Ffv1AviReader(args.input, device=dev)
+    else:
+        rd = pio.open_reader(args.input)
     W, H = (int(v) for v in args.size.split("x"))
     target = formats.fmt(args.pix_fmt)
     rate = Fraction(args.fps) if args.fps else rd.rate
@@ -110,14 +114,21 @@ def cmd_avpvs(args):
         stage = Stage(rd.fmt, rd.w, rd.h, target, W, H, lambda s, d, st: sc(s, d, stream=st))
     fb = formats.frame_bytes(target, W, H)
     cap = int(round(float(args.duration) * float(rate))) if args.duration else None
-    inner = _open_writer(out, target, W, H, rate, args.vopts, args.aopts,
-                         None if args.aopts.strip() == "-an" else args.input, args.y)
+    if args.gpu_ffv1:
+        # the AVPVS as FFV1 encoded on the GPU, in an AVI written here (video
+        # only: the reference's -c:a flac track needs ffmpeg, see _mux_audio)
+        from .ffv1 import Ffv1AviWriter
+        inner = Ffv1AviWriter(out, target, W, H, rate, device=dev)
+    else:
+        inner = _open_writer(out, target, W, H, rate, args.vopts, args.aopts,
+                             None if args.aopts.strip() == "-an" else args.input, args.y)
     stall = None
     if args.stall_output:
         # create_avpvs_short of a PVS with stalls: compose the stalled AVPVS
         # (the bufferer step's output) from the frames this pass writes
         stall = _StallOutput(args.stall_output, target, W, H, rate, args.buffer, args.skipping, args.spinner,
-                             args.black_frame, args.stall_vopts, args.stall_aopts, args.input, True, dev)
+                             args.black_frame, args.stall_vopts, args.stall_aopts, args.input, True, dev,
+                             gpu_ffv1=args.gpu_ffv1)
         inner = _Tee(inner, stall.push, fb)
     wr = CountingWriter(inner, fb, cap)
     emit = _fps_counts(rd.rate, rate) if args.fps else None
@@ -127,6 +138,8 @@ def cmd_avpvs(args):
             wr.write(wr.last)
     rd.close()
     wr.close()
+    if args.gpu_ffv1:
+        _mux_audio(out, args.input, args.aopts)
     if stall is not None:
         import json
         stall.close()
@@ -134,6 +147,24 @@ def cmd_avpvs(args):
             json.dump(_stall_record(out, args.buffer, args.skipping, args.spinner, args.black_frame, args.pix_fmt,
                                     args.stall_vopts, args.stall_aopts), f)
     return 0
+
+
+def _mux_audio(video_avi, audio_src, aopts):
+    """Add the source's audio to a video-only AVI with the reference's audio
+    options (e.g. `-c:a flac`), stream-copying the GPU-encoded FFV1; without
+    ffmpeg (or with -an) the AVI stays video-only."""
+    import shutil
+    import subprocess
+    if aopts.strip() == "-an" or not shutil.which("ffmpeg"):
+        if aopts.strip() != "-an":
+            print("pixpath: no ffmpeg: %s written without audio" % video_avi, file=sys.stderr)
+        return
+    tmp = video_avi + ".video.avi"  # pragma: no cover - needs ffmpeg
+    os.replace(video_avi, tmp)
+    cmd = ["ffmpeg", "-nostdin", "-v", "error", "-y", "-i", tmp, "-i", audio_src, "-map", "0:v", "-map", "1:a?",
+           "-c:v", "copy"] + aopts.split() + [video_avi]
+    subprocess.run(cmd, check=True)
+    os.remove(tmp)
 
 
 class _Tee:
@@ -197,7 +228,11 @@ def cmd_cpvs(args):
         return 0
     dev = _device()
     torch.cuda.set_device(dev)
-    rd = pio.open_reader(args.input)
+    if args.gpu_ffv1:  # an FFV1 AVPVS written by `avpvs --gpu-ffv1`: decoded on the GPU
+        from .ffv1 import Ffv1AviReader
+        rd = Ffv1AviReader(args.input, device=dev)
+    else:
+        rd = pio.open_reader(args.input)
     W, H = (rd.w, rd.h) if not args.pad else (int(v) for v in args.pad.split("x"))
     W, H = int(W), int(H)
     cur_fmt = rd.fmt
@@ -270,7 +305,7 @@ class _StallOutput:
     the AVPVS writer itself, no second decode)."""
 
     def __init__(self, out, fmt, w, h, rate, buffer, skipping, spinner_path, black_frame, vopts, aopts,
-                 audio_input, overwrite, dev):
+                 audio_input, overwrite, dev, gpu_ffv1=False):
         import torch
         from . import io as pio, ops, spinner
         from .frames import FrameBatch
@@ -282,13 +317,18 @@ class _StallOutput:
             anim, delays = spinner.load_apng(spinner_path)
             ops.spinner_upload(anim, fmt, device=dev)
         audio_from, graph = None, None
+        if gpu_ffv1:  # FFV1 encoded on the GPU into an AVI (video only, as `avpvs --gpu-ffv1`)
+            from .ffv1 import Ffv1AviWriter
+            aopts = "-an"
         if aopts.strip() != "-an" and os.path.splitext(out)[1].lower() not in (".y4m", ".raw", ".yuv"):
             ap = pio.audio_params(audio_input)  # pragma: no cover - needs ffprobe
             if ap is not None:
                 audio_from = audio_input
                 if not skipping:
                     graph = stall_audio_graph(stall_times(events, rate), ap[0], ap[1])
-        if audio_from:  # pragma: no cover - needs ffmpeg
+        if gpu_ffv1:
+            self.wr = Ffv1AviWriter(out, fmt, w, h, rate, device=dev)
+        elif audio_from:  # pragma: no cover - needs ffmpeg
             self.wr = pio.FFmpegWriter(out, fmt, w, h, rate, vopts, aopts, audio_from=audio_from,
                                        overwrite="-y" if overwrite else "-n", audio_filter=graph)
         else:
@@ -375,9 +415,13 @@ def cmd_stall(args):
         return 0
     dev = _device()
     torch.cuda.set_device(dev)
-    rd = pio.open_reader(args.input)
+    if args.gpu_ffv1:
+        from .ffv1 import Ffv1AviReader
+        rd = Ffv1AviReader(args.input, device=dev)
+    else:
+        rd = pio.open_reader(args.input)
     so = _StallOutput(out, rd.fmt, rd.w, rd.h, rd.rate, args.buffer, args.skipping, args.spinner, args.black_frame,
-                      args.vopts, args.aopts, args.input, args.y, dev)
+                      args.vopts, args.aopts, args.input, args.y, dev, gpu_ffv1=args.gpu_ffv1)
     buf = np.empty((1, rd.frame_bytes), np.uint8)
     while rd.read_into(buf, 1) == 1:
         so.push.push(buf[0].copy())
@@ -436,6 +480,8 @@ def main(argv=None):
     p.add_argument("--black-frame", action="store_true")
     p.add_argument("--stall-vopts", default="-c:v ffv1")
     p.add_argument("--stall-aopts", default="-c:a pcm_s16le")
+    p.add_argument("--gpu-ffv1", action="store_true", help="FFV1 encoded on the GPU into an AVI (pixpath.avi)")
+    p.add_argument("--ffv1-input", action="store_true", help="input is a --gpu-ffv1 AVI: decode it on the GPU")
     p.set_defaults(fn=cmd_avpvs)
 
     p = sub.add_parser("encseg")
@@ -458,6 +504,7 @@ def main(argv=None):
     p.add_argument("--vcodec", required=True)
     p.add_argument("--pix-fmt", required=True)
     p.add_argument("--pad", default=None)
+    p.add_argument("--gpu-ffv1", action="store_true", help="input is an FFV1 AVI: decode it on the GPU")
     p.set_defaults(fn=cmd_cpvs)
 
     p = sub.add_parser("stall")
@@ -467,6 +514,7 @@ def main(argv=None):
     p.add_argument("--spinner", default=None)
     p.add_argument("--skipping", action="store_true")
     p.add_argument("--black-frame", action="store_true")
+    p.add_argument("--gpu-ffv1", action="store_true", help="FFV1 AVI in and out, coded on the GPU")
     p.set_defaults(fn=cmd_stall)
 
     p = sub.add_parser("siti")

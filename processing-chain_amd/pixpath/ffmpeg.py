@@ -70,6 +70,16 @@ def _skip_existing(output_file, overwrite):
 
 
 def _gpu_cli(sub, args):
+    args = list(args)
+    if os.environ.get("PIXPATH_FFV1") == "gpu":
+        # FFV1 AVPVS coded on the GPU in pixpath's own AVI (opt-in):
+        # the AVPVS writers encode it, its readers (CPVS, stall, mobile scale) decode it
+        if sub == "avpvs" and FFV1_OPTS in args:
+            args.insert(-1, "--gpu-ffv1")
+        elif sub == "avpvs":
+            args.insert(-1, "--ffv1-input")
+        elif sub in ("cpvs", "stall"):
+            args.insert(-1, "--gpu-ffv1")
     return "PYTHONPATH={} python3 -m pixpath.cli {} {}".format(shlex.quote(PKG_DIR), sub,
                                                                 " ".join(shlex.quote(str(a)) for a in args))
 

@@ -110,3 +110,74 @@ class Ffv1Decoder:
                                    sizes.ctypes.data_as(ctypes.c_void_p), n, ctypes.byref(s),
                                    _stream(dst.planes[0], stream)))
         return dst
+
+
+class Ffv1AviWriter:
+    """`cli avpvs --gpu-ffv1`: the AVPVS written as FFV1 encoded on the GPU in
+    an AVI (pixpath.avi) -- the `-c:v ffv1 ... <pvs>.avi` of lib/ffmpeg.py:993
+    without ffmpeg's encoder.  Takes dense host frames (the pipeline's writer
+    interface), encodes them in batches."""
+
+    def __init__(self, path, fmt, w, h, rate, slices=(8, 8), batch=64, device=None):
+        from . import avi
+        from .frames import FrameBatch
+        self.fmt = formats.fmt(fmt)
+        self.fb = formats.frame_bytes(self.fmt, w, h)
+        self.batch = int(batch)
+        self.enc = Ffv1Encoder(self.fmt, w, h, slices=slices, max_frames=self.batch, device=device)
+        dev = torch.device("cuda", self.enc.ctx.device)
+        self.stage = FrameBatch.interleaved(self.fmt, w, h, self.batch, device=dev)
+        self.avi = avi.AviWriter(path, w, h, rate, extradata=self.enc.extradata)
+
+    def write(self, frames_u8):
+        from .frames import FrameBatch
+        data = np.frombuffer(memoryview(frames_u8).cast("B"), np.uint8)
+        n = len(data) // self.fb
+        for i in range(0, n, self.batch):
+            k = min(self.batch, n - i)
+            self.stage.storage[:k].copy_(torch.from_numpy(data[i * self.fb:(i + k) * self.fb].reshape(k, self.fb)))
+            src = FrameBatch.interleaved(self.fmt, self.enc.w, self.enc.h, k, device=self.stage.device,
+                                         storage=self.stage.storage[:k])
+            for p in self.enc.encode_to_host(src):
+                self.avi.write_packet(p)
+
+    def close(self):
+        self.avi.close()
+
+
+class Ffv1AviReader:
+    """`cli cpvs --gpu-ffv1`: an FFV1 AVI (as Ffv1AviWriter writes it) read
+    back through the GPU decoder; the reader interface of pixpath.io."""
+
+    def __init__(self, path, batch=64, device=None):
+        from . import avi
+        info, self.packets = avi.read_packets(path)
+        if info.get("fourcc") != b"FFV1":
+            raise ValueError("%s: not an FFV1 AVI" % path)
+        self.w, self.h, self.rate = info["w"], info["h"], info["rate"]
+        self.batch = int(batch)
+        self.dec = Ffv1Decoder(info["extradata"], self.w, self.h, max_frames=self.batch, device=device)
+        self.fmt = self.dec.fmt
+        self.pos = 0
+
+    @property
+    def frame_bytes(self):
+        return formats.frame_bytes(self.fmt, self.w, self.h)
+
+    def read_into(self, buf, n):
+        """Decode up to n frames into the dense host array buf [n, frame_bytes]; returns the count."""
+        from .frames import FrameBatch
+        k = min(n, len(self.packets) - self.pos)
+        done = 0
+        while done < k:
+            m = min(self.batch, k - done)
+            pk = self.packets[self.pos:self.pos + m]
+            out = FrameBatch.interleaved(self.fmt, self.w, self.h, m, device=torch.device("cuda", self.dec.ctx.device))
+            self.dec.decode(b"".join(pk), [len(p) for p in pk], dst=out)
+            buf[done:done + m] = out.storage[:m].cpu().numpy()
+            self.pos += m
+            done += m
+        return k
+
+    def close(self):
+        pass

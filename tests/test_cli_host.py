@@ -93,3 +93,16 @@ def test_gpu_avpvs_short_composes_stalls_in_the_same_pass(monkeypatch):
     monkeypatch.delenv("PIXPATH_SPINNER")
     monkeypatch.setattr(pff, "default_spinner_path", lambda: None)
     assert "--stall-output" not in pff.create_avpvs_short(pvs, overwrite=True)
+
+
+def test_gpu_ffv1_opt_in_flags(monkeypatch):
+    """PIXPATH_FFV1=gpu: AVPVS writers encode FFV1 on the GPU, AVPVS readers decode it there."""
+    from pixpath import ffmpeg as pff
+    monkeypatch.setenv("PIXPATH_FFV1", "gpu")
+    a = pff._gpu_cli("avpvs", ["-y", "--vopts", pff.FFV1_OPTS, "/o.avi"])
+    assert a.endswith("--gpu-ffv1 /o.avi")
+    assert pff._gpu_cli("avpvs", ["-y", "--vopts", "-c:v libx264", "/o.mp4"]).endswith("--ffv1-input /o.mp4")
+    assert pff._gpu_cli("cpvs", ["-y", "/c.avi"]).endswith("--gpu-ffv1 /c.avi")
+    assert pff._gpu_cli("stall", ["-y", "/s.avi"]).endswith("--gpu-ffv1 /s.avi")
+    monkeypatch.delenv("PIXPATH_FFV1")
+    assert "--gpu-ffv1" not in pff._gpu_cli("cpvs", ["-y", "/c.avi"])

@@ -4,6 +4,8 @@ and decoded back to the input by the oracle's decoder (lossless; the slice
 CRCs and FFmpeg's end-of-slice position check pass).  Parity against FFmpeg
 itself is unpinned (no FFV1 implementation exists in this container or on
 the box)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -131,3 +133,64 @@ def test_gpu_decode_600_frames(gpu):
     out = dec.decode(buf.cpu().numpy().tobytes(), sizes)
     for p in range(3):
         assert torch.equal(out.view(p)[:n], src.view(p)[:n])
+
+
+def test_cli_avpvs_cpvs_through_gpu_ffv1(gpu, tmp_path):
+    """create_avpvs_short -> create_cpvs with the FFV1 AVPVS encoded and decoded
+    on the GPU (`--gpu-ffv1`): the AVI holds FFV1 packets the C restatement
+    decodes to the oracle's scaled frames, and the CPVS read back from it
+    equals the oracle's pad + v210 of those frames."""
+    from fractions import Fraction
+    from pixpath import avi, cli, io as pio
+    rng = np.random.default_rng(12)
+    frames = [synth.noise_frame(rng, po.YUV422P10LE, 640, 360) for _ in range(70)]
+    seg, avpvs, cpvs = (str(tmp_path / n) for n in ("seg.y4m", "avpvs.avi", "cpvs.raw"))
+    wr = pio.Y4MWriter(seg, "yuv422p10le", 640, 360, 60)
+    wr.write(pio.join_planes(synth.batch(frames)))
+    wr.close()
+    assert cli.main(["avpvs", "-y", "--input", seg, "--size", "1280x720", "--pix-fmt", "yuv422p10le",
+                     "--aopts=-an", "--gpu-ffv1", "--batch", "32", avpvs]) == 0
+    info, pk = avi.read_packets(avpvs)
+    assert (info["w"], info["h"], info["rate"], len(pk)) == (1280, 720, Fraction(60), 70)
+    want = [po.scale(po.YUV422P10LE, f, po.YUV422P10LE, 1280, 720, po.SWS_BICUBIC) for f in frames]
+    for j in (0, 33, 69):
+        rc, dec = ref.decode_frame(info["extradata"], pk[j], 1280, 720, 10, 1, 0)
+        assert rc == 0
+        for p in range(3):
+            np.testing.assert_array_equal(dec[p], want[j][p])
+    assert cli.main(["cpvs", "-y", "--input", avpvs, "--fps", "60", "--vcodec", "v210", "--pix-fmt", "yuv422p10le",
+                     "--pad", "1280x800", "--gpu-ffv1", cpvs]) == 0
+    raw = np.fromfile(cpvs, np.uint8)
+    fb = po.v210_linesize(1280) * 800
+    assert raw.size == 70 * fb
+    for j in (0, 69):
+        ref_v210 = po.v210_pack(po.pad(po.YUV422P10LE, want[j], 1280, 800, 0, 40))
+        np.testing.assert_array_equal(raw[j * fb:(j + 1) * fb], ref_v210.reshape(-1))
+
+
+def test_cli_stall_through_gpu_ffv1(gpu, tmp_path):
+    """The stall path with FFV1 AVIs coded on the GPU: the fused pass
+    (`avpvs --stall-output --gpu-ffv1`) and the bufferer step on the AVPVS AVI
+    (`stall --gpu-ffv1`) give the same frames."""
+    from pixpath import avi, cli, io as pio
+    rng = np.random.default_rng(13)
+    frames = [synth.noise_frame(rng, po.YUV420P, 320, 180) for _ in range(30)]
+    seg, wo, fused, plain = (str(tmp_path / n) for n in ("seg.y4m", "wo.avi", "pvs.avi", "plain.avi"))
+    wr = pio.Y4MWriter(seg, "yuv420p", 320, 180, 60)
+    wr.write(pio.join_planes(synth.batch(frames)))
+    wr.close()
+    spinner = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "spinner-128-white.png")
+    buf = "[[0.1,0.1],[0.4,0.05]]"
+    assert cli.main(["avpvs", "-y", "--input", seg, "--size", "640x360", "--pix-fmt", "yuv420p", "--aopts=-an",
+                     "--gpu-ffv1", "--stall-output", fused, "--buffer", buf, "--black-frame", "--spinner", spinner,
+                     wo]) == 0
+    assert cli.main(["stall", "-y", "--input", wo, "--buffer", buf, "--pix-fmt", "yuv420p", "--black-frame",
+                     "--spinner", spinner, "--vopts", "-c:v ffv1", "--aopts=-an", "--gpu-ffv1", plain]) == 0
+    (i1, p1), (i2, p2) = avi.read_packets(fused), avi.read_packets(plain)
+    assert len(p1) == len(p2) == 30 + 6 + 3
+    for a_, b_ in zip(p1, p2):
+        r1, d1 = ref.decode_frame(i1["extradata"], a_, 640, 360, 8, 1, 1)
+        r2, d2 = ref.decode_frame(i2["extradata"], b_, 640, 360, 8, 1, 1)
+        assert r1 == r2 == 0
+        for p in range(3):
+            np.testing.assert_array_equal(d1[p], d2[p])
