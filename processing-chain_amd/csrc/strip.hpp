@@ -31,9 +31,28 @@
 
 namespace pp {
 
-constexpr int kStripPF = 3;  // 16-B staging chunks per lane prefetched into registers
+// 16-B staging chunks per lane prefetched into registers: 3 covers the new
+// source rows of an upscale chunk; 16-bit sources with wide H windows (HW >= 8:
+// downscales, ~2 new source rows per output row) get PIXPATH_STRIP_PF_WIDE so
+// the staging of a chunk is not mostly synchronous loads in commit()
+// (config 3, 2160p yuv422p10le -> 1080p: 5.94 -> 4.82 ms; 8-bit sources stage
+// 16 samples per chunk and lose slightly with 6: 3.32 -> 3.40 ms)
+#ifndef PIXPATH_STRIP_PF_WIDE
+#define PIXPATH_STRIP_PF_WIDE 6
+#endif
+#ifndef PIXPATH_STRIP_PF_U8_WIDE
+#define PIXPATH_STRIP_PF_U8_WIDE 3
+#endif
+#ifndef PIXPATH_STRIP_PF_NARROW
+#define PIXPATH_STRIP_PF_NARROW 3
+#endif
+template <int HW, int SB>
+constexpr int strip_pf() {
+    return HW >= 8 ? (SB == 2 ? PIXPATH_STRIP_PF_WIDE : PIXPATH_STRIP_PF_U8_WIDE) : PIXPATH_STRIP_PF_NARROW;
+}
+template <int PF>
 struct StripPrefetch {
-    uint4 v[kStripPF];
+    uint4 v[PF];
 };
 
 // Waves per SIMD the register allocation is bounded for: 6 (80 VGPRs, the LDS
@@ -41,7 +60,7 @@ struct StripPrefetch {
 // else 4 (128 VGPRs) or 3 (168 VGPRs, the widest H windows).  tools/check_spills.sh checks every instance.
 template <int SB, int OUTB, int HW, int VTM>
 constexpr int strip_min_waves() {
-    return HW >= 12 ? 3 : (VTM <= 5 && HW <= (OUTB == 10 && SB == 2 ? 6 : 4)) ? 6 : 4;
+    return HW >= 10 ? 3 : (VTM <= 5 && HW <= (OUTB == 10 && SB == 2 ? 6 : 4)) ? 6 : 4;
 }
 
 // 4 adjacent outputs of a row at column xo (8-bit bytes or 16-bit samples)
@@ -151,7 +170,8 @@ __global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)siz
     const bool s_on = s_r0 < s_rstep;
     const int s_lds = s_r0 * S + s_ch * CH;
     const int s_goff = s_r0 * (int)sls + cbyte + s_ch * 16;
-    auto prefetch = [&](StripPrefetch &pf, int from, int hi_) {
+    constexpr int kStripPF = strip_pf<HW, (int)sizeof(ST)>();
+    auto prefetch = [&](StripPrefetch<kStripPF> &pf, int from, int hi_) {
         const int nrow = hi_ - from;
 #pragma unroll
         for (int k = 0; k < kStripPF; ++k) {
@@ -159,7 +179,7 @@ __global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)siz
             pf.v[k] = bload16(rs, (s_on && r < nrow) ? s_goff + (from + k * s_rstep) * (int)sls : kOobOff);
         }
     };
-    auto commit = [&](const StripPrefetch &pf, int from, int hi_) {
+    auto commit = [&](const StripPrefetch<kStripPF> &pf, int from, int hi_) {
         const int nrow = hi_ - from;
         if (!s_on) return;
 #pragma unroll
@@ -194,7 +214,7 @@ __global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)siz
     const int cho = J.cho;
     int next_src = chunk_lo[y_begin / cho];
     int base = next_src & ~1;
-    StripPrefetch pf;
+    StripPrefetch<kStripPF> pf;
     // the first chunk's rows are staged before the loop; every later chunk's
     // rows are loaded right after the chunk-start barrier of the chunk before
     // and written to LDS right after its window barrier (src_t is free then).
