@@ -449,30 +449,28 @@ __device__ __forceinline__ void siti_range(const uint8_t *frames, int64_t ls, in
     if (pend) reduce_store(f1 - 1, true, p_K, p_l1, p_l2, p_d1, p_d2, p_hp);
 }
 
-// 1-D grid sized to the resident workgroup slots; workgroup i walks the
-// (tile, frame) units [i*U/G, (i+1)*U/G) in tile-major order -- equal work per
-// workgroup (fixed frame chunks per band would leave slots idle whenever the
-// band count does not divide them) and at most one band switch per range.
-// XCD-aware: an XCD holds consecutive ranges, i.e. adjacent bands advancing
-// through the same frames together, so the halo rows they share hit its L2.
+// 1-D grid sized to the resident workgroup slots.  The frames are cut into
+// chunks of `fchunk` and the (chunk, tile) units are numbered chunk-major;
+// workgroup L takes units L, L + G, L + 2G, ...  So the workgroups running at
+// any moment hold vertically adjacent bands of the SAME frames, and with the
+// XCD-aware numbering (consecutive L on one XCD) a band's two halo rows are
+// read from HBM by one neighbour and hit that XCD's L2 for the other.  The
+// host picks fchunk so that the rounds of units fill the slots (see pp_siti).
 template <typename T, bool RAGGED>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void siti_kernel(
     const uint8_t *frames, int64_t ls, int64_t fs, int nframes, const uint8_t *prev, int W, int H, int tiles_x,
-    int ntiles, SitiPartial *part) {
-    const int64_t total = (int64_t)ntiles * nframes;
-    const int L = xcd_remap(blockIdx.x, gridDim.x);
-    int64_t u = total * L / gridDim.x;
-    const int64_t u1 = total * (L + 1) / gridDim.x;
-    while (u < u1) {
-        const int tile = (int)(u / nframes);
-        const int f0 = (int)(u - (int64_t)tile * nframes);
-        const int f1 = (int)min<int64_t>(nframes, f0 + (u1 - u));
+    int ntiles, int fchunk, SitiPartial *part) {
+    const int chunks = (nframes + fchunk - 1) / fchunk;
+    const int64_t total = (int64_t)ntiles * chunks;
+    for (int64_t u = xcd_remap(blockIdx.x, gridDim.x); u < total; u += gridDim.x) {
+        const int chunk = (int)(u / ntiles);
+        const int tile = (int)(u - (int64_t)chunk * ntiles);
+        const int f0 = chunk * fchunk, f1 = min(nframes, f0 + fchunk);
         const int y0 = tile / tiles_x * kBand;
         if (y0 >= 1 && y0 + kBand + 1 <= H)
             siti_range<T, true, RAGGED>(frames, ls, fs, prev, W, H, tiles_x, tile, f0, f1, part);
         else
             siti_range<T, false, RAGGED>(frames, ls, fs, prev, W, H, tiles_x, tile, f0, f1, part);
-        u += f1 - f0;
     }
 }
 
@@ -532,7 +530,8 @@ extern "C" int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma
     const int bands = (h + kBand - 1) / kBand;
     const int ntiles = tiles_x * bands;
     const bool ragged = (w % kLanePx) != 0;
-    using KFn = void (*)(const uint8_t *, int64_t, int64_t, int, const uint8_t *, int, int, int, int, SitiPartial *);
+    using KFn = void (*)(const uint8_t *, int64_t, int64_t, int, const uint8_t *, int, int, int, int, int,
+                         SitiPartial *);
     const KFn k = bytes == 2 ? (ragged ? siti_kernel<uint16_t, true> : siti_kernel<uint16_t, false>)
                              : (ragged ? siti_kernel<uint8_t, true> : siti_kernel<uint8_t, false>);
     const void *kfn = reinterpret_cast<const void *>(k);
@@ -542,7 +541,22 @@ extern "C" int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma
     PP_HIP(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     PP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, 0));
     const int64_t slots = std::max(1, dev_cus * std::max(1, per_cu));
-    const int groups = (int)std::min<int64_t>(slots, (int64_t)ntiles * nframes);
+    // frames per chunk: for R = 1..8 rounds of units over the slots, the
+    // longest chunk that still fits R rounds; keep the R with the shortest
+    // makespan (R * fchunk frames, plus ~1 frame of pipeline fill per round)
+    int fchunk = nframes;
+    {
+        double best = 1e300;
+        for (int R = 1; R <= 8; ++R) {
+            const int K = (int)std::max<int64_t>(1, std::min<int64_t>(nframes, R * slots / ntiles));
+            const int fc = (nframes + K - 1) / K;
+            const int64_t units = (int64_t)ntiles * ((nframes + fc - 1) / fc);
+            const int64_t rounds = (units + std::min(slots, units) - 1) / std::min(slots, units);
+            const double cost = (double)rounds * (fc + 1);
+            if (cost < best) { best = cost; fchunk = fc; }
+        }
+    }
+    const int groups = (int)std::min<int64_t>(slots, (int64_t)ntiles * ((nframes + fchunk - 1) / fchunk));
     // The kernel reads each lane's 8 pixels as one 16-B (8-B) buffer load, so
     // rows must start on that granule; other layouts (odd widths packed
     // contiguously, views into a row) are first repacked on the device into a
@@ -583,7 +597,8 @@ extern "C" int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma
         src = dst;
         psrc = prev ? scratch : nullptr;
     }
-    hipLaunchKernelGGL(k, dim3(groups), dim3(256), 0, st, src, ls, fs, nframes, psrc, w, h, tiles_x, ntiles, part);
+    hipLaunchKernelGGL(k, dim3(groups), dim3(256), 0, st, src, ls, fs, nframes, psrc, w, h, tiles_x, ntiles, fchunk,
+                       part);
     hipLaunchKernelGGL(siti_finalize, dim3(nframes), dim3(256), 0, st, part, nframes, ntiles * 4, w, h,
                        prev != nullptr, si, ti);  // ntiles * 4 wave partials per frame
     PP_HIP(hipGetLastError());
