@@ -14,7 +14,8 @@
 // shuffles (global loads only at wave edges), and slides a 3-row window down
 // the band, so every pixel of the band is read from HBM once per frame; the
 // previous frame's band (TI) stays in registers (16 rows x 8 px packed in 64
-// VGPRs), only the two halo rows are read twice.
+// VGPRs); only the two halo rows are read twice, the second time from L2
+// (the neighbouring band runs the same frames on the same XCD, see siti_kernel).
 // Precision: |G| = sqrt in fp32; per lane and frame the shifted sums
 // S1 = sum(|G| - K), S2 = sum(|G| - K)^2 in fp32, K being one of the lane's own
 // samples of that frame (so S2 - S1^2/n cancels at most ~n eps, ~1e-5 relative,
