@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--launches", type=int, default=3)
     ap.add_argument("--frames", type=int, default=600)
     ap.add_argument("--flags", default="lanczos")
+    ap.add_argument("--src", default="yuv422p10le:1280x720", help="source fmt:WxH (config 3: yuv420p:3840x2160)")
     a = ap.parse_args()
     import torch
     from pixpath import ops
@@ -26,12 +27,15 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(910)
     if a.which in ("scale", "both"):
-        src = FrameBatch("yuv422p10le", 1280, 720, n, device=dev)
+        sfmt, wh = a.src.split(":")
+        sw, sh = (int(t) for t in wh.split("x"))
+        hi = 941 if "10" in sfmt else 236
+        src = FrameBatch(sfmt, sw, sh, n, device=dev)
         for p in range(3):
             v = src.view(p)
-            v.copy_(torch.randint(64, 941, v.shape, generator=g, device=dev, dtype=torch.int32).to(torch.uint16))
+            v.copy_(torch.randint(16, hi, v.shape, generator=g, device=dev, dtype=torch.int32).to(v.dtype))
         dst = FrameBatch("yuv422p10le", 1920, 1080, n, device=dev)
-        sc = ops.Scaler("yuv422p10le", 1280, 720, "yuv422p10le", 1920, 1080, flags=a.flags)
+        sc = ops.Scaler(sfmt, sw, sh, "yuv422p10le", 1920, 1080, flags=a.flags)
         for _ in range(a.launches):
             sc(src, dst)
         torch.cuda.synchronize()
