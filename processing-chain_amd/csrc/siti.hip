@@ -29,7 +29,7 @@
 // Bound: VALU, not HBM -- the interior frame loop is ~1660 VALU instructions
 // per wave and frame for 8 x 16 pixels a lane (per pixel: two op_sel'd
 // v_pk_mad_i16 build (h1, h2), two more give (gx, gy), one v_dot2 |G|^2, one
-// v_sqrt_f32; TI by v_dot2), 0.65 ms on config 2
+// v_sqrt_f32; TI by v_dot2), 0.63-0.65 ms on config 2
 // (profiles/r2/siti_experiments.md).
 #include <algorithm>
 #include <cmath>
