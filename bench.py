@@ -8,9 +8,9 @@ Unit of work = one PVS of BASELINE config 2: a 10 s 1080p60 SRC ->
 A step = every rank runs its share of a batch of PVSes (pixpath.batch.my_pvs,
 the reference's ParallelRunner unit, lib/cmd_utils.py:93-101), then the
 per-frame SI/TI of every PVS is gathered to rank 0 on the host (gloo).  Inputs
-are resident in HBM when the timed region starts.  Defaults: 32 PVS per rank
-(weak scaling), so 8 ranks run BASELINE config 5 (256 PVS = 153,600 frames);
---pvs-total 256 runs config 5 at any rank count.
+are resident in HBM when the timed region starts.  Default: BASELINE config 5,
+a fixed batch of 256 PVS (153,600 frames) split over the ranks (strong
+scaling); --pvs-per-rank K instead gives every rank K PVS (weak scaling).
 value = frames of that workload per second over all ranks (each frame gets
 both its AVPVS upscale and its SI/TI).
 
@@ -67,18 +67,20 @@ def frame_bytes(fmt, w, h):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)  # ~2 s timed at 1 GPU: long enough for a busy sampler to see the GPU
+    ap.add_argument("--steps", type=int, default=20)  # ~11 s timed at 1 GPU (config 5: 256 PVS per step)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=FRAMES, help="frames per PVS")
-    ap.add_argument("--pvs-per-rank", type=int, default=32)
-    ap.add_argument("--pvs-total", type=int, default=None, help="fixed batch size (strong scaling), e.g. 256")
+    ap.add_argument("--pvs-per-rank", type=int, default=None, help="PVS per rank (weak scaling)")
+    ap.add_argument("--pvs-total", type=int, default=256, help="fixed batch (strong scaling): config 5 = 256")
     ap.add_argument("--pool", type=int, default=8, help="distinct resident PVS inputs per rank")
     ap.add_argument("--workload", default="config2", choices=sorted(list(WORKLOADS) + ["config4", "ffv1"]))
     ap.add_argument("--ffv1-slices", default="8x8", help="FFV1 slice grid (workload ffv1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="per CPU-baseline stage")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU-baseline stage at full width")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every thread of the affinity mask")
+    ap.add_argument("--cpu-sweep", default="16,64", help="extra thread counts timed (shorter) beside the full width")
+    ap.add_argument("--no-siti-file", action="store_true")
     return ap.parse_args()
 
 
@@ -98,31 +100,47 @@ def host_cpu():
     return model, os.cpu_count(), aff
 
 
+def cgroup_cpus():
+    """CPU quota of this cgroup (cpu.max) in CPUs, or None when unlimited/unknown."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(args, wl):
     """Oracle C restatement on host threads (ctypes releases the GIL); the
     scaler and SI/TI are timed separately, the combined rate is per frame that
-    gets both (1 / (1/scale + 1/siti))."""
+    gets both (1 / (1/scale + 1/siti)).  `value` is the rate on EVERY thread of
+    the affinity mask; a shorter sweep over fewer threads is recorded beside."""
     import threading
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as po
     sfmt, sw, sh, dfmt, dw, dh, flags, siti_wh = wl
     model, nproc, aff = host_cpu()
-    nt = max(1, min(args.cpu_threads, aff))
+    full = args.cpu_threads or aff
     rng = np.random.default_rng(910)
     sf, df = po.FMT_BY_NAME[sfmt], po.FMT_BY_NAME[dfmt]
     depth = po.fmt_info(sf)[0]
     hi = 1024 if depth > 8 else 256
+    # 16 distinct read-only inputs shared by the threads (each has its own Sws scratch)
     src = [[rng.integers(0, hi, s).astype(po.plane_dtype(sf)) for s in po.plane_shapes(sf, sw, sh)]
-           for _ in range(nt)]
+           for _ in range(16)]
     fl = {"lanczos": po.SWS_LANCZOS, "bicubic": po.SWS_BICUBIC}[flags]
-    sws = [po.Sws(sf, sw, sh, df, dw, dh, fl) for _ in range(nt)]
+    sws = [po.Sws(sf, sw, sh, df, dw, dh, fl) for _ in range(full)]
+    outs = [x.out_planes() for x in sws]
+    luma = None
+    if siti_wh:
+        w, h = siti_wh
+        luma = [rng.integers(0, 1024, (4, h, w)).astype(np.uint16) for _ in range(16)]
 
-    def timed(fn):
+    def timed(fn, nt, secs):
         done = [0] * nt
 
         def work(t):
-            while time.perf_counter() - t0 < args.cpu_seconds:
+            while time.perf_counter() - t0 < secs:
                 done[t] += fn(t)
         t0 = time.perf_counter()
         th = [threading.Thread(target=work, args=(t,)) for t in range(nt)]
@@ -133,32 +151,75 @@ def cpu_baseline(args, wl):
         return sum(done), time.perf_counter() - t0
 
     def do_scale(t):
-        sws[t].scale(src[t])
-        return 1
-    ns, ts = timed(do_scale)
-    scale_fps = ns / ts
-    out = {"unit": "frames/s", "cores": nt, "kind": "port", "host_nproc": nproc, "host_affinity": aff,
-           "cpu_model": model, "scale_fps": round(scale_fps, 2)}
-    if siti_wh:
-        w, h = siti_wh
-        luma = [rng.integers(0, 1024, (8, h, w)).astype(np.uint16) for _ in range(nt)]
+        sws[t].scale_into(src[t % 16], outs[t], 4)  # 4 frames per C call
+        return 4
 
-        def do_siti(t):
-            po.siti_c(luma[t], 10)  # 8 frames: 8 SI + 7 TI
-            return 8
-        nq, tq = timed(do_siti)
-        siti_fps = nq / tq
-        out["siti_fps"] = round(siti_fps, 2)
-        out["value"] = round(1.0 / (1.0 / scale_fps + 1.0 / siti_fps), 2)
-        out["sample"] = ("%d-thread oracle C restatement (oracle/pixoracle.c + siti_oracle.c, gcc -O3): %d frames "
-                         "%dx%d %s -> %dx%d %s %s in %.1f s, then %d frames of %dx%d 10-bit SI/TI in %.1f s; "
-                         "value = per frame that gets both; ffmpeg is absent on the box"
-                         % (nt, ns, sw, sh, sfmt, dw, dh, dfmt, flags, ts, nq, w, h, tq))
+    def do_siti(t):
+        po.siti_c(luma[t % 16], 10)  # 4 frames: 4 SI + 3 TI
+        return 4
+
+    def point(nt, secs):
+        ns, ts = timed(do_scale, nt, secs)
+        r = {"threads": nt, "scale_fps": round(ns / ts, 2), "scale_frames": ns, "scale_s": round(ts, 2)}
+        if siti_wh:
+            nq, tq = timed(do_siti, nt, secs)
+            r.update(siti_fps=round(nq / tq, 2), siti_frames=nq, siti_s=round(tq, 2))
+            r["value"] = round(1.0 / (1.0 / r["scale_fps"] + 1.0 / r["siti_fps"]), 2)
+        else:
+            r["value"] = r["scale_fps"]
+        return r
+
+    sweep = [point(k, max(2.0, args.cpu_seconds / 2)) for k in
+             sorted({int(v) for v in args.cpu_sweep.split(",") if v.strip() and 0 < int(v) < full})]
+    top = point(full, args.cpu_seconds)
+    out = {"value": top["value"], "unit": "frames/s", "cores": full, "kind": "port", "host_nproc": nproc,
+           "host_affinity": aff, "cgroup_cpus": cgroup_cpus(), "cpu_model": model,
+           "scale_fps": top["scale_fps"], "sweep": sweep + [top]}
+    if siti_wh:
+        out["siti_fps"] = top["siti_fps"]
+        out["sample"] = ("%d-thread oracle C restatement (oracle/pixoracle.c + siti_oracle.c, gcc -O3; every thread of "
+                         "the affinity mask): %d frames %dx%d %s -> %dx%d %s %s in %.1f s, then %d frames of %dx%d "
+                         "10-bit SI/TI in %.1f s; value = per frame that gets both; ffmpeg is absent on the box"
+                         % (full, top["scale_frames"], sw, sh, sfmt, dw, dh, dfmt, flags, top["scale_s"],
+                            top["siti_frames"], siti_wh[0], siti_wh[1], top["siti_s"]))
     else:
-        out["value"] = round(scale_fps, 2)
         out["sample"] = ("%d-thread oracle C restatement (gcc -O3): %d frames %dx%d %s -> %dx%d %s %s in %.1f s; "
-                         "ffmpeg is absent on the box" % (nt, ns, sw, sh, sfmt, dw, dh, dfmt, flags, ts))
+                         "ffmpeg is absent on the box" % (full, top["scale_frames"], sw, sh, sfmt, dw, dh, dfmt, flags,
+                                                         top["scale_s"]))
     return out
+
+
+def siti_file(dev, n=600, w=1920, h=1080):
+    """The SRC-analysis SI/TI hook on a file: a 600-frame 1080p yuv422p10le Y4M
+    (written to the temp dir first, so it is in the page cache) through
+    pixpath.siti.siti_of_file -- luma-only read, pinned double buffers, H2D
+    overlapped with the kernel.  File -> per-frame SI/TI on the host."""
+    import tempfile
+    import numpy as np
+    from pixpath import formats, io as pio, siti
+    fb = formats.frame_bytes("yuv422p10le", w, h)
+    rng = np.random.default_rng(600)
+    pool = [rng.integers(64, 941, fb // 2).astype(np.uint16).view(np.uint8) for _ in range(4)]
+    d = tempfile.mkdtemp(prefix="pixpath_bench_")
+    path = os.path.join(d, "src.y4m")
+    try:
+        wr = pio.Y4MWriter(path, "yuv422p10le", w, h, 60)
+        for i in range(n):
+            wr.write(pool[i % 4])
+        wr.close()
+        siti.siti_of_file(path, batch=120)  # warm-up (pinned buffers, kernel load)
+        t0 = time.perf_counter()
+        si, ti = siti.siti_of_file(path, batch=120)
+        dt = time.perf_counter() - t0
+    finally:
+        if os.path.exists(path):
+            os.remove(path)
+        os.rmdir(d)
+    assert len(si) == n
+    return {"frames_per_s": round(n / dt, 1), "frames": n, "seconds": round(dt, 3),
+            "luma_gbs": round(n * w * h * 2 / dt / 1e9, 2),
+            "note": "600-frame 1080p yuv422p10le Y4M (page cache) -> luma-only read -> pinned double buffers -> "
+                    "H2D (copy stream) -> siti_kernel (compute stream) -> per-frame SI/TI on the host"}
 
 
 def pcie_pipeline(wl, n_frames, dev):
@@ -244,7 +305,7 @@ def main():
     wl = WORKLOADS[args.workload]
     sfmt, sw, sh, dfmt, dw, dh, flags, siti_wh = wl
     n = args.frames
-    total = args.pvs_total or world * args.pvs_per_rank
+    total = world * args.pvs_per_rank if args.pvs_per_rank else args.pvs_total
     ids = ["PVS%03d" % i for i in range(total)]
     mine = batch.my_pvs(ids, rank, world)
     k_pool = max(1, min(args.pool, len(mine)))
@@ -319,7 +380,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1000.0 / args.steps, 4),
         "higher_is_better": True,
-        "scaling": "strong" if args.pvs_total else "weak",
+        "scaling": "weak" if args.pvs_per_rank else "strong",
         "vs_baseline": None,
         "dtype": "u16",
         "data": "synthetic (seeded legal-range samples generated in HBM; %d distinct resident PVS inputs per rank)"
@@ -356,6 +417,8 @@ def main():
                                                                    "TI": round(some["TI"], 4)}}
     if world == 1 and not args.no_pipeline:
         out["pcie_pipeline"] = pcie_pipeline(wl, 600, dev)
+    if world == 1 and siti_wh and not args.no_siti_file:
+        out["siti_file"] = siti_file(dev)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, wl)
     print(json.dumps(out), flush=True)

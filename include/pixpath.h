@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PP_ABI_VERSION 3
+#define PP_ABI_VERSION 4
 
 /* return codes */
 #define PP_OK 0
@@ -177,6 +177,14 @@ int pp_stall_compose(pp_ctx *ctx, int fmt, int w, int h, const pp_frames *src,
 int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma,
             int64_t linesize, int64_t frame_stride, int nframes,
             const void *prev, double *si, double *ti, void *stream);
+/* pp_siti with flags: PP_SITI_NORMALIZE divides SI_n and TI_n by
+ * 2^(bitdepth-8) (SURVEY.md 8a-13's optional normalisation), so 8- and 10-bit
+ * SRCs report on the 8-bit scale; an exact power-of-two scaling of the raw
+ * values.  pp_siti(...) == pp_siti_ex(..., 0, stream). */
+#define PP_SITI_NORMALIZE 1
+int pp_siti_ex(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma,
+               int64_t linesize, int64_t frame_stride, int nframes,
+               const void *prev, double *si, double *ti, int flags, void *stream);
 
 /* ---- host helpers --------------------------------------------------------
  * vf_fps output->input frame map (lib/ffmpeg.py:832-834, :959-961, :1038,

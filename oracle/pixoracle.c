@@ -667,3 +667,19 @@ int po_fps_map(int n_in, int64_t in_num, int64_t in_den, int64_t out_num, int64_
     }
     return (int)n_out;
 }
+
+/*
+ * Timing helper for bench.py's cpu_baseline leg: po_sws_scale of one frame
+ * `count` times in one call, so a Python thread per core spends its time in C
+ * (the GIL is released for the whole call by ctypes).  Returns 0 or the first
+ * failure.
+ */
+int po_sws_scale_n(const po_sws *c, const uint8_t *const src[3], const int64_t sls[3],
+                   uint8_t *const dst[3], const int64_t dls[3], int count)
+{
+    for (int i = 0; i < count; i++) {
+        int rc = po_sws_scale(c, src, sls, dst, dls);
+        if (rc) return rc;
+    }
+    return 0;
+}

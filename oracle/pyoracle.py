@@ -63,6 +63,7 @@ def lib():
         L.po_sws_get_filter.argtypes = [vp, ctypes.c_int, vp, vp]
         L.po_sws_filter_size.argtypes = [vp, ctypes.c_int]
         L.po_sws_scale.argtypes = [vp, vp, vp, vp, vp]
+        L.po_sws_scale_n.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int]
         L.po_init_filter.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int)] + [ctypes.c_int] * 6 + \
             [ctypes.c_double] * 2 + [ctypes.c_int] * 2
         L.po_pad.argtypes = [ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int, vp, vp] + [ctypes.c_int] * 4
@@ -152,6 +153,16 @@ class Sws:
         if rc:
             raise RuntimeError("po_sws_scale failed")
         return outs[:1] if self.dst_fmt == UYVY422 else outs
+
+    def out_planes(self):
+        """Output planes for scale_into (planar destination formats)."""
+        return [np.zeros(s, dtype=plane_dtype(self.dst_fmt)) for s in plane_shapes(self.dst_fmt, self.dw, self.dh)]
+
+    def scale_into(self, planes, outs, count=1):
+        """Scale the same frame `count` times into preallocated planar `outs`
+        (bench.py's cpu_baseline: one C call per batch, no per-frame Python)."""
+        if lib().po_sws_scale_n(self._h, _ptrs(planes), _lses(planes), _ptrs(outs), _lses(outs), int(count)):
+            raise RuntimeError("po_sws_scale failed")
 
 
 def scale(src_fmt, planes, dst_fmt, dw, dh, flags=SWS_BICUBIC, p0=PARAM_DEFAULT, p1=PARAM_DEFAULT):

@@ -52,11 +52,13 @@ def ti_frame(y, prev):
     return float(np.std(d.astype(np.float64)))
 
 
-def siti(frames, prev=None):
+def siti(frames, prev=None, bitdepth=None, normalize=False):
     """Per-frame (si, ti) arrays for a [N, H, W] luma stack.
 
     ``prev`` is the frame preceding frames[0] (a 1-frame halo when a long SRC
-    is split across workers), else TI_0 is NaN.
+    is split across workers), else TI_0 is NaN.  ``normalize`` (with
+    ``bitdepth``): both divided by 2^(bitdepth-8), the optional 8-bit-scale
+    normalisation of SURVEY.md 8a-13 (PP_SITI_NORMALIZE).
     """
     frames = np.asarray(frames)
     n = frames.shape[0]
@@ -66,6 +68,9 @@ def siti(frames, prev=None):
         si[i] = si_frame(frames[i])
         p = frames[i - 1] if i else prev
         ti[i] = ti_frame(frames[i], p) if p is not None else np.nan
+    if normalize:
+        k = 1.0 / (1 << (int(bitdepth) - 8))
+        si, ti = si * k, ti * k
     return si, ti
 
 

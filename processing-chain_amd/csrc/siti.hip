@@ -479,7 +479,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void s
 // then a fixed-shape LDS tree -- the order never depends on timing, so the
 // result is bit-reproducible.
 __global__ __launch_bounds__(256) void siti_finalize(const SitiPartial *part, int nframes, int nparts, int W, int H,
-                                                     int has_prev, double *si, double *ti) {
+                                                     int has_prev, double scale, double *si, double *ti) {
     __shared__ double s_mean[256], s_m2[256];
     __shared__ int64_t s_n[256], s_d1[256];
     __shared__ uint64_t s_d2[256];
@@ -503,14 +503,15 @@ __global__ __launch_bounds__(256) void siti_finalize(const SitiPartial *part, in
         __syncthreads();
     }
     if (t) return;
-    si[f] = s_n[0] ? sqrt(s_m2[0] / static_cast<double>(s_n[0])) : 0.0;
+    // scale: 1, or 2^-(bitdepth-8) with PP_SITI_NORMALIZE (an exact power of two)
+    si[f] = s_n[0] ? sqrt(s_m2[0] / static_cast<double>(s_n[0])) * scale : 0.0;
     if (f == 0 && !has_prev) {
         ti[f] = __builtin_nan("");
     } else {
         const int64_t np = static_cast<int64_t>(W) * H;
         const __int128 num = static_cast<__int128>(np) * static_cast<__int128>(s_d2[0]) -
                              static_cast<__int128>(s_d1[0]) * static_cast<__int128>(s_d1[0]);
-        ti[f] = sqrt(static_cast<double>(num)) / static_cast<double>(np);
+        ti[f] = sqrt(static_cast<double>(num)) / static_cast<double>(np) * scale;
     }
 }
 
@@ -520,6 +521,13 @@ using namespace pp;
 
 extern "C" int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma, int64_t linesize,
                        int64_t frame_stride, int nframes, const void *prev, double *si, double *ti, void *stream) {
+    return pp_siti_ex(ctx, bitdepth, w, h, luma, linesize, frame_stride, nframes, prev, si, ti, 0, stream);
+}
+
+extern "C" int pp_siti_ex(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma, int64_t linesize,
+                          int64_t frame_stride, int nframes, const void *prev, double *si, double *ti, int flags,
+                          void *stream) {
+    if (flags & ~PP_SITI_NORMALIZE) PP_FAIL(PP_ERR_INVALID, "siti flags 0x%x", flags);
     if (!ctx || !luma || !si || !ti || nframes < 0) PP_FAIL(PP_ERR_INVALID, "null argument");
     if (bitdepth != 8 && bitdepth != 10) PP_FAIL(PP_ERR_INVALID, "bit depth %d (8 or 10)", bitdepth);
     if (w < 3 || h < 3) PP_FAIL(PP_ERR_INVALID, "frame %dx%d too small for Sobel", w, h);
@@ -601,7 +609,8 @@ extern "C" int pp_siti(pp_ctx *ctx, int bitdepth, int w, int h, const void *luma
     hipLaunchKernelGGL(k, dim3(groups), dim3(256), 0, st, src, ls, fs, nframes, psrc, w, h, tiles_x, ntiles, fchunk,
                        part);
     hipLaunchKernelGGL(siti_finalize, dim3(nframes), dim3(256), 0, st, part, nframes, ntiles * 4, w, h,
-                       prev != nullptr, si, ti);  // ntiles * 4 wave partials per frame
+                       prev != nullptr, (flags & PP_SITI_NORMALIZE) ? 1.0 / (double)(1 << (bitdepth - 8)) : 1.0, si,
+                       ti);  // ntiles * 4 wave partials per frame
     PP_HIP(hipGetLastError());
     PP_HIP(hipFreeAsync(part, st));
     if (scratch) PP_HIP(hipFreeAsync(scratch, st));

@@ -17,7 +17,7 @@ EXPORTS = (
     "pp_abi_version", "pp_last_error", "pp_ctx_create", "pp_ctx_destroy", "pp_plane_bytes",
     "pp_v210_linesize", "pp_scale_plan_create", "pp_scale_chain_plan_create", "pp_scale_plan_destroy", "pp_scale_plan_filter",
     "pp_scale_plan_path", "pp_scale_plan_stats", "pp_scale_execute", "pp_pad_execute", "pp_v210_pack", "pp_cpvs_execute", "pp_spinner_upload", "pp_stall_compose",
-    "pp_siti", "pp_fps_map",
+    "pp_siti", "pp_siti_ex", "pp_fps_map",
     "pp_device_alloc", "pp_device_free", "pp_host_alloc", "pp_host_free", "pp_stream_create",
     "pp_stream_destroy", "pp_stream_synchronize", "pp_event_create", "pp_event_destroy", "pp_event_record",
     "pp_stream_wait_event", "pp_event_synchronize", "pp_event_elapsed_ms", "pp_copy_async", "pp_copy2d_async",
@@ -27,6 +27,7 @@ EXPORTS = (
 )
 PP_COPY_H2D, PP_COPY_D2H, PP_COPY_D2D = 1, 2, 3
 PP_NAL_H264, PP_NAL_H265 = 1, 2
+PP_SITI_NORMALIZE = 1
 
 
 class NativeMissing(RuntimeError):
@@ -78,6 +79,7 @@ def lib():
         "pp_spinner_upload": (i32, [vp, i32, vp, i32, i32, i32]),
         "pp_stall_compose": (i32, [vp, i32, i32, i32, fr, vp, vp, fr, i32, vp]),
         "pp_siti": (i32, [vp, i32, i32, i32, vp, i64, i64, i32, vp, vp, vp, vp]),
+        "pp_siti_ex": (i32, [vp, i32, i32, i32, vp, i64, i64, i32, vp, vp, vp, i32, vp]),
         "pp_fps_map": (i32, [i32, i64, i64, i64, i64, vp, i32]),
         "pp_device_alloc": (i32, [vp, i64, ctypes.POINTER(vp)]),
         "pp_device_free": (i32, [vp, vp]),

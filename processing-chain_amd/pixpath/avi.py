@@ -129,28 +129,61 @@ class AviWriter:
         self.fh.close()
 
 
-def read_packets(path):
-    """(info, packets): info = {w, h, rate, fourcc, extradata}; packets in order."""
-    info, packets = {}, []
+def scan(path):
+    """(info, index) of an AVI without loading it: info = {w, h, rate,
+    handler, fourcc, extradata} of its first VIDEO stream ('vids' strl; an
+    audio strl's strh/strf never overwrite it), index = [(file offset, size)]
+    of that stream's packets in file order.  Chunks are walked with seeks, so
+    a tens-of-GB long-test AVPVS costs one 8-byte read per packet."""
+    info, index = {}, []
     with open(path, "rb") as fh:
-        data = fh.read()
+        fh.seek(0, 2)
+        total = fh.tell()
+        state = {"strl": -1, "type": None, "video": None}
 
-    def walk(pos, end):
-        while pos + 8 <= end:
-            tag, size = data[pos:pos + 4], struct.unpack_from("<I", data, pos + 4)[0]
-            body = pos + 8
-            if tag in (b"RIFF", b"LIST"):
-                walk(body + 4, body + size)
-            elif tag == b"strh":
-                scale, rate = struct.unpack_from("<II", data, body + 20)
-                info["rate"] = Fraction(rate, scale)
-                info["handler"] = data[body + 4:body + 8]
-            elif tag == b"strf":
-                bi_size, w, h = struct.unpack_from("<Iii", data, body)
-                info.update(w=w, h=abs(h), fourcc=data[body + 16:body + 20], extradata=data[body + 40:body + bi_size])
-            elif tag[2:] in (b"dc", b"db") and tag[:2].isdigit():
-                packets.append(data[body:body + size])
-            pos = body + size + (size & 1)
+        def walk(pos, end):
+            while pos + 8 <= end:
+                fh.seek(pos)
+                hdr = fh.read(12)
+                if len(hdr) < 8:
+                    return
+                tag, size = hdr[:4], struct.unpack_from("<I", hdr, 4)[0]
+                body = pos + 8
+                if tag in (b"RIFF", b"LIST"):
+                    if hdr[8:12] == b"strl":
+                        state["strl"] += 1
+                        state["type"] = None
+                    walk(body + 4, min(body + size, end))
+                elif tag == b"strh":
+                    fh.seek(body)
+                    d = fh.read(min(size, 56))
+                    state["type"] = d[:4]
+                    if d[:4] == b"vids" and state["video"] is None:
+                        state["video"] = state["strl"]
+                        scale, rate = struct.unpack_from("<II", d, 20)
+                        info["rate"] = Fraction(rate, scale)
+                        info["handler"] = d[4:8]
+                elif tag == b"strf":
+                    if state["type"] == b"vids" and state["strl"] == state["video"] and "w" not in info:
+                        fh.seek(body)
+                        d = fh.read(size)
+                        bi_size, w, h = struct.unpack_from("<Iii", d, 0)
+                        info.update(w=w, h=abs(h), fourcc=d[16:20], extradata=d[40:bi_size])
+                elif tag[2:] in (b"dc", b"db") and tag[:2].isdigit():
+                    if state["video"] is not None and int(tag[:2]) == state["video"]:
+                        index.append((body, size))
+                pos = body + size + (size & 1)
 
-    walk(0, len(data))
+        walk(0, total)
+    return info, index
+
+
+def read_packets(path):
+    """(info, packets): scan() plus the packet bytes, in order (small files / tests)."""
+    info, index = scan(path)
+    with open(path, "rb") as fh:
+        packets = []
+        for off, size in index:
+            fh.seek(off)
+            packets.append(fh.read(size))
     return info, packets

@@ -21,7 +21,6 @@ unit stays the PVS and the pool becomes one process per GPU:
 import os
 import socket
 import subprocess
-import sys
 
 import numpy as np
 
@@ -116,38 +115,3 @@ def gather_results(local, rank, world):
             out[k] = {"si": si, "ti": ti, "SI": float(si.max()) if si.size else float("nan"),
                       "TI": float(valid.max()) if valid.size else float("nan"), "rank": r}
     return out
-
-
-# ---- CPU self-test of the launcher (tests/test_distributed_gloo.py) ----------
-def _selftest_frames(pvs_index):
-    rng = np.random.default_rng(1000 + pvs_index)
-    return rng.integers(0, 1024, (5, 24, 40)).astype(np.uint16)
-
-
-def _selftest(out_path, n_pvs):
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
-                                    "oracle"))
-    import siti_ref
-    rank, world, _ = rank_env()
-    init_group(world)
-    ids = ["PVS%03d" % i for i in range(n_pvs)]
-    local = {}
-    for pid in my_pvs(ids, rank, world):
-        local[pid] = siti_ref.siti(_selftest_frames(int(pid[3:])))
-    res = gather_results(local, rank, world)
-    if rank == 0:
-        np.savez(out_path, ids=np.array(sorted(res)), world=world,
-                 ranks=np.array([res[k]["rank"] for k in sorted(res)]),
-                 SI=np.array([res[k]["SI"] for k in sorted(res)]), TI=np.array([res[k]["TI"] for k in sorted(res)]),
-                 si=np.stack([res[k]["si"] for k in sorted(res)]), ti=np.stack([res[k]["ti"] for k in sorted(res)]))
-    barrier(world)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
-
-
-if __name__ == "__main__":
-    if len(sys.argv) >= 3 and sys.argv[1] == "--selftest":
-        _selftest(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 6)
-    else:
-        sys.exit("usage: python -m pixpath.batch --selftest OUT.npz [N_PVS]")

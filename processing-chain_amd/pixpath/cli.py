@@ -440,7 +440,7 @@ def _black(fmt, w, h):
 
 def cmd_siti(args):
     from . import siti
-    si, ti = siti.siti_of_file(args.input, batch=args.batch)
+    si, ti = siti.siti_of_file(args.input, batch=args.batch, normalize=args.normalize)
     SI, TI = siti.siti_summary(si, ti)
     res = {"file": os.path.basename(args.input), "si": SI, "ti": TI, "frames": int(len(si))}
     if args.per_frame:
@@ -521,6 +521,7 @@ def main(argv=None):
     p.add_argument("--input", required=True)
     p.add_argument("--batch", type=int, default=120)
     p.add_argument("--per-frame", action="store_true")
+    p.add_argument("--normalize", action="store_true", help="SI/TI on the 8-bit scale (/ 2^(bitdepth-8))")
     p.set_defaults(fn=cmd_siti)
 
     args = ap.parse_args(argv)

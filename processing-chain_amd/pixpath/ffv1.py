@@ -100,7 +100,10 @@ class Ffv1Decoder:
 
     def decode(self, packets, sizes, dst=None, stream=None):
         from .frames import FrameBatch
-        data = np.frombuffer(bytes(packets) if not isinstance(packets, (bytes, bytearray)) else packets, np.uint8)
+        if isinstance(packets, np.ndarray):
+            data = np.ascontiguousarray(packets, dtype=np.uint8)
+        else:
+            data = np.frombuffer(bytes(packets) if not isinstance(packets, (bytes, bytearray)) else packets, np.uint8)
         sizes = np.ascontiguousarray(sizes, dtype=np.int64)
         n = len(sizes)
         if dst is None:
@@ -147,11 +150,14 @@ class Ffv1AviWriter:
 
 class Ffv1AviReader:
     """`cli cpvs --gpu-ffv1`: an FFV1 AVI (as Ffv1AviWriter writes it) read
-    back through the GPU decoder; the reader interface of pixpath.io."""
+    back through the GPU decoder; the reader interface of pixpath.io.  Only
+    the packet index is held (pixpath.avi.scan); each batch's packets are read
+    from the file when that batch is decoded, so a long-test AVPVS of tens of
+    GB never sits in host memory."""
 
-    def __init__(self, path, batch=64, device=None):
+    def __init__(self, path, batch=256, device=None):
         from . import avi
-        info, self.packets = avi.read_packets(path)
+        info, self.index = avi.scan(path)
         if info.get("fourcc") != b"FFV1":
             raise ValueError("%s: not an FFV1 AVI" % path)
         self.w, self.h, self.rate = info["w"], info["h"], info["rate"]
@@ -159,25 +165,52 @@ class Ffv1AviReader:
         self.dec = Ffv1Decoder(info["extradata"], self.w, self.h, max_frames=self.batch, device=device)
         self.fmt = self.dec.fmt
         self.pos = 0
+        self.fh = open(path, "rb")
 
     @property
     def frame_bytes(self):
         return formats.frame_bytes(self.fmt, self.w, self.h)
 
-    def read_into(self, buf, n):
-        """Decode up to n frames into the dense host array buf [n, frame_bytes]; returns the count."""
+    def __len__(self):
+        return len(self.index)
+
+    def _read(self, i, m):
+        """Packets i..i+m-1 back to back (one read of their file span) and their sizes."""
+        ent = self.index[i:i + m]
+        lo, hi = ent[0][0], ent[-1][0] + ent[-1][1]
+        self.fh.seek(lo)
+        span = np.frombuffer(self.fh.read(hi - lo), np.uint8)
+        sizes = np.array([s for _, s in ent], np.int64)
+        if hi - lo == int(sizes.sum()):
+            return span, sizes
+        return np.concatenate([span[o - lo:o - lo + s] for o, s in ent]), sizes
+
+    def read_device(self, n):
+        """Decode up to n frames into an interleaved device FrameBatch (None at the end)."""
         from .frames import FrameBatch
-        k = min(n, len(self.packets) - self.pos)
+        k = min(n, len(self.index) - self.pos)
+        if k <= 0:
+            return None
+        out = FrameBatch.interleaved(self.fmt, self.w, self.h, k, device=torch.device("cuda", self.dec.ctx.device))
         done = 0
         while done < k:
             m = min(self.batch, k - done)
-            pk = self.packets[self.pos:self.pos + m]
-            out = FrameBatch.interleaved(self.fmt, self.w, self.h, m, device=torch.device("cuda", self.dec.ctx.device))
-            self.dec.decode(b"".join(pk), [len(p) for p in pk], dst=out)
-            buf[done:done + m] = out.storage[:m].cpu().numpy()
+            data, sizes = self._read(self.pos, m)
+            part = FrameBatch.interleaved(self.fmt, self.w, self.h, m, device=out.device,
+                                          storage=out.storage[done:done + m])
+            self.dec.decode(data, sizes, dst=part)
             self.pos += m
             done += m
+        return out
+
+    def read_into(self, buf, n):
+        """Decode up to n frames into the dense host array buf [n, frame_bytes]; returns the count."""
+        out = self.read_device(n)
+        if out is None:
+            return 0
+        k = out.n
+        buf[:k] = out.storage[:k].cpu().numpy()
         return k
 
     def close(self):
-        pass
+        self.fh.close()

@@ -263,6 +263,77 @@ class SelectReader(Reader):
         self.inner.close()
 
 
+class LumaReader:
+    """The luma plane of every frame, nothing else (P.910 SI/TI reads luma
+    only): Y4M / raw files seek past the chroma planes; any other container
+    is decoded by ffmpeg straight to `-pix_fmt gray` / `gray10le`, so the
+    decode pipe, the pinned buffers and PCIe carry 1/2 (4:2:2) or 2/3 (4:2:0)
+    fewer bytes than full frames.  read_into(buf, n) fills n dense
+    [h * w * bytes_per_sample] luma frames."""
+
+    def __init__(self, path, f=None, w=None, h=None, rate=None):
+        """path: a file name, or an open binary Y4M stream (e.g. a pipe)."""
+        ext = os.path.splitext(path)[1].lower() if isinstance(path, str) else ".y4m"
+        self.proc = None
+        self.skip = 0
+        if ext == ".y4m":
+            y = Y4MReader(path)
+            self.fh, fmt, self.w, self.h, self.rate = y.fh, y.fmt, y.w, y.h, y.rate
+            self.y4m = True
+        elif ext in (".raw", ".yuv"):
+            fmt = formats.fmt(f)
+            self.fh, self.w, self.h, self.rate = open(path, "rb"), int(w), int(h), Fraction(rate or 60)
+            self.y4m = False
+        else:  # pragma: no cover - needs ffmpeg
+            st = probe(path)["stream"]
+            fmt = formats.fmt(f or st["pix_fmt"]) if (f or st["pix_fmt"]) in formats.NAMES else None
+            depth = fmt.depth if fmt else (10 if "10" in st["pix_fmt"] else 8)
+            self.w, self.h = int(w or st["width"]), int(h or st["height"])
+            self.rate = Fraction(rate or st["r_frame_rate"])
+            self.proc = subprocess.Popen(["ffmpeg", "-nostdin", "-v", "error", "-i", path, "-f", "rawvideo",
+                                          "-pix_fmt", "gray10le" if depth > 8 else "gray", "pipe:1"],
+                                         stdout=subprocess.PIPE, bufsize=1 << 24)
+            self.fh, self.y4m, self.depth = self.proc.stdout, False, depth
+        if self.proc is None:
+            self.depth = fmt.depth
+            self.skip = formats.frame_bytes(fmt, self.w, self.h) - self.luma_bytes
+        try:
+            self.seekable = self.fh.seekable()
+        except (AttributeError, OSError):
+            self.seekable = False
+        self._scratch = None if self.seekable else bytearray(self.skip)
+
+    @property
+    def luma_bytes(self):
+        return self.w * self.h * (2 if self.depth > 8 else 1)
+
+    def read_into(self, buf, n):
+        lb = self.luma_bytes
+        mv = memoryview(buf).cast("B")
+        got = 0
+        while got < n:
+            if self.y4m:
+                line = self.fh.readline()
+                if not line:
+                    break
+                if not line.startswith(b"FRAME"):
+                    raise ValueError("bad Y4M frame header")
+            if _readexact(self.fh, mv[got * lb:(got + 1) * lb]) != lb:
+                break
+            if self.skip:
+                if self.seekable:
+                    self.fh.seek(self.skip, os.SEEK_CUR)
+                else:
+                    _readexact(self.fh, memoryview(self._scratch))
+            got += 1
+        return got
+
+    def close(self):
+        self.fh.close()
+        if self.proc is not None and self.proc.wait():  # pragma: no cover - needs ffmpeg
+            raise RuntimeError("ffmpeg decode failed")
+
+
 def open_reader(path, f=None, w=None, h=None, rate=None, start=None, duration=None):
     """Reader for a Y4M / raw file (read directly) or any container (ffmpeg
     decode pipe); start/duration trim like `-ss start -i path -t duration`."""

@@ -167,10 +167,11 @@ def cpvs(src, W=None, H=None, out_fmt=None, x=-1, y=-1, dst=None, stream=None):
     return dst
 
 
-def siti(luma, bitdepth, prev=None, stream=None):
+def siti(luma, bitdepth, prev=None, stream=None, normalize=False):
     """Per-frame P.910 SI/TI of a [N, H, W] luma tensor (uint8 / uint16, may be a
     pitched view).  Returns two float64 device tensors [N]; ti[0] is NaN when
-    ``prev`` (the frame before luma[0]) is not given."""
+    ``prev`` (the frame before luma[0]) is not given.  ``normalize``: values
+    divided by 2^(bitdepth-8) (the 8-bit scale, PP_SITI_NORMALIZE)."""
     if luma.dim() != 3:
         raise ValueError("luma must be [N, H, W]")
     n, h, w = luma.shape
@@ -185,9 +186,9 @@ def siti(luma, bitdepth, prev=None, stream=None):
         if prev.stride(-1) != 1 or prev.stride(-2) != luma.stride(1):
             raise ValueError("prev must share the luma row pitch")
         pp = ctypes.c_void_p(prev.data_ptr())
-    check(lib().pp_siti(ctx.handle, int(bitdepth), w, h, ctypes.c_void_p(luma.data_ptr()), luma.stride(1) * es,
-                        luma.stride(0) * es, n, pp, ctypes.c_void_p(si.data_ptr()),
-                        ctypes.c_void_p(ti.data_ptr()), _stream(luma, stream)))
+    check(lib().pp_siti_ex(ctx.handle, int(bitdepth), w, h, ctypes.c_void_p(luma.data_ptr()), luma.stride(1) * es,
+                           luma.stride(0) * es, n, pp, ctypes.c_void_p(si.data_ptr()),
+                           ctypes.c_void_p(ti.data_ptr()), 1 if normalize else 0, _stream(luma, stream)))
     return si, ti
 
 

@@ -1,13 +1,16 @@
 """Host<->device streaming pipeline: pinned double buffers + async copies.
 
-decode pipe --read--> pinned_in[k%2] --H2D (copy stream)--> dev_in[k%2]
-   --kernels (compute stream)--> dev_out[k%2] --D2H (copy stream)--> pinned_out[k%2]
+decode pipe --read--> pinned_in[k%2] --H2D (h2d stream)--> dev_in[k%2]
+   --kernels (compute stream)--> dev_out[k%2] --D2H (d2h stream)--> pinned_out[k%2]
    --write--> encode pipe
 
 Reading batch k+1 and writing batch k-1 (host threads) overlap the H2D,
-kernels and D2H of batch k; the copy engine and the compute queue are
-separate HIP streams ordered by events, so PCIe traffic overlaps the kernels of
-the neighbouring batch.  Frame layout everywhere is dense Y|U|V per frame.
+kernels and D2H of batch k.  H2D, compute and D2H are three HIP streams
+ordered by events only where a buffer is reused, so the two PCIe directions
+run concurrently (batch k+1's upload beside batch k-1's download) and both
+overlap the kernels.  A writer with ``write_device(batch, stream)`` takes the
+device output directly (the GPU FFV1 encoder): no D2H, no re-upload.  Frame
+layout everywhere is dense Y|U|V per frame.
 """
 import queue
 import threading
@@ -40,7 +43,8 @@ class Pipeline:
         self.h_out = [torch.empty((B, self.out_fb), dtype=torch.uint8).pin_memory() for _ in range(2)]
         self.d_in = [FrameBatch.interleaved(s.in_fmt, s.in_w, s.in_h, B, device=self.device) for _ in range(2)]
         self.d_out = [FrameBatch.interleaved(s.out_fmt, s.out_w, s.out_h, B, device=self.device) for _ in range(2)]
-        self.copy_stream = torch.cuda.Stream(self.device)
+        self.h2d_stream = torch.cuda.Stream(self.device)
+        self.d2h_stream = torch.cuda.Stream(self.device)
         self.compute_stream = torch.cuda.Stream(self.device)
         self.frames_in = self.frames_out = 0
 
@@ -97,6 +101,8 @@ class Pipeline:
         out_free = [threading.Event(), threading.Event()]
         for e in out_free:
             e.set()
+        comp_done, d2h_done = [None, None], [None, None]
+        device_writer = hasattr(writer, "write_device")
         tr = threading.Thread(target=read_loop, daemon=True)
         tw = threading.Thread(target=write_loop, daemon=True)
         tr.start()
@@ -113,34 +119,57 @@ class Pipeline:
                 free_in.put(slot)
                 break
             out_free[slot].clear()
-            with torch.cuda.stream(self.copy_stream):
+            with torch.cuda.stream(self.h2d_stream):
+                if comp_done[slot] is not None:  # batch k-2's kernels have read dev_in[slot]
+                    self.h2d_stream.wait_event(comp_done[slot])
                 self.d_in[slot].storage[:n].copy_(self.h_in[slot][:n], non_blocking=True)
                 h2d_done = torch.cuda.Event()
-                h2d_done.record(self.copy_stream)
+                h2d_done.record(self.h2d_stream)
             self.compute_stream.wait_event(h2d_done)
+            if d2h_done[slot] is not None:  # batch k-2's download has read dev_out[slot]
+                self.compute_stream.wait_event(d2h_done[slot])
             with torch.cuda.stream(self.compute_stream):
                 src = FrameBatch.interleaved(self.stage.in_fmt, self.stage.in_w, self.stage.in_h, n,
                                              device=self.device, storage=self.d_in[slot].storage[:n])
                 dst = FrameBatch.interleaved(self.stage.out_fmt, self.stage.out_w, self.stage.out_h, n,
                                              device=self.device, storage=self.d_out[slot].storage[:n])
                 self.stage.process(src, dst, self.compute_stream)
-                comp_done = torch.cuda.Event()
-                comp_done.record(self.compute_stream)
-            self.copy_stream.wait_event(comp_done)
-            with torch.cuda.stream(self.copy_stream):
+                comp_done[slot] = torch.cuda.Event()
+                comp_done[slot].record(self.compute_stream)
+            if device_writer:
+                # the writer consumes the device batch on the compute stream (e.g. FFV1 encode)
+                writer.write_device(dst, self.compute_stream, emit=None if emit is None else
+                                    [emit(base + i) for i in range(n)])
+                d2h_ev = torch.cuda.Event()
+                d2h_ev.record(self.compute_stream)
+                d2h_done[slot] = d2h_ev
+                h2d_done.synchronize()
+                free_in.put(slot)
+                out_free[slot].set()
+                self.frames_in += n
+                self.frames_out += n
+                base += n
+                if n < B:
+                    break
+                continue
+            self.d2h_stream.wait_event(comp_done[slot])
+            with torch.cuda.stream(self.d2h_stream):
                 self.h_out[slot][:n].copy_(self.d_out[slot].storage[:n], non_blocking=True)
-                d2h_done = torch.cuda.Event()
-                d2h_done.record(self.copy_stream)
+                d2h_ev = torch.cuda.Event()
+                d2h_ev.record(self.d2h_stream)
+            d2h_done[slot] = d2h_ev
             # the input slot can be refilled once its H2D copy has finished
             h2d_done.synchronize()
             free_in.put(slot)
-            wq.put((slot, n, d2h_done, base))
+            wq.put((slot, n, d2h_ev, base))
             self.frames_in += n
             base += n
             if n < B:
                 break
         wq.put(None)
         tw.join()
+        if device_writer:
+            self.compute_stream.synchronize()
         tr.join(timeout=1.0)
         if err:
             raise err[0]

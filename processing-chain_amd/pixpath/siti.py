@@ -51,9 +51,10 @@ def sum_file(videofile, ordernum):
     return "md5sum file written for file: {}".format(base)
 
 
-def siti_of_batch(luma, bitdepth, prev=None):
+def siti_of_batch(luma, bitdepth, prev=None, normalize=False):
     """Per-frame SI/TI (numpy float64 arrays) of a [N, H, W] luma batch on the GPU.
-    ``luma`` may be a numpy array or a (device) torch tensor."""
+    ``luma`` may be a numpy array or a (device) torch tensor.  ``normalize``:
+    values on the 8-bit scale (divided by 2^(bitdepth-8), PP_SITI_NORMALIZE)."""
     import torch
 
     from . import ops
@@ -64,7 +65,7 @@ def siti_of_batch(luma, bitdepth, prev=None):
     if prev is not None:
         p = prev if isinstance(prev, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(prev))
         p = p.to(t.device)
-    si, ti = ops.siti(t, bitdepth, prev=p)
+    si, ti = ops.siti(t, bitdepth, prev=p, normalize=normalize)
     torch.cuda.current_stream(t.device).synchronize()
     return si.cpu().numpy(), ti.cpu().numpy()
 
@@ -76,37 +77,152 @@ def siti_summary(si, ti):
     return float(np.max(si)) if len(si) else float("nan"), float(np.max(ti)) if ti.size else float("nan")
 
 
-def siti_of_file(videofile, batch=120, reader=None):
-    """Decode a file (ffmpeg, or y4m/raw via pixpath.io) and return per-frame SI/TI."""
+def siti_of_file(videofile, batch=120, reader=None, normalize=False, with_depth=False):
+    """Per-frame SI/TI of a file: decoded luma only (pixpath.io.LumaReader:
+    y4m/raw seek past chroma, ffmpeg decodes to gray/gray10le), streamed
+    through pinned double buffers (siti_stream).  ``reader``: a full-frame
+    pixpath.io reader instead (its luma plane is used).  Returns (si, ti) or,
+    with_depth, (si, ti, bitdepth)."""
     from . import io as pio
-    rd = reader or pio.open_reader(videofile)
-    sis, tis, prev = [], [], None
-    for frames in rd.batches(batch):
-        luma = frames[0]
-        si, ti = siti_of_batch(luma, rd.fmt.depth, prev=prev)
-        sis.append(si)
-        tis.append(ti)
-        prev = luma[-1]
-    rd.close()
-    return np.concatenate(sis), np.concatenate(tis)
+    if reader is not None:
+        rd = _LumaOf(reader)
+    else:
+        rd = pio.LumaReader(videofile)
+    try:
+        si, ti = siti_stream(rd, batch=batch, normalize=normalize)
+    finally:
+        rd.close()
+    return (si, ti, rd.depth) if with_depth else (si, ti)
 
 
-def siti_yaml_entry(si, ti):
-    """The extra "siti" key of <src>.yaml (spec PP-SITI-1)."""
+class _LumaOf:
+    """A full-frame pixpath.io reader seen as a luma reader."""
+
+    def __init__(self, rd):
+        self.rd, self.w, self.h, self.depth = rd, rd.w, rd.h, rd.fmt.depth
+        self.luma_bytes = self.w * self.h * (2 if self.depth > 8 else 1)
+        self._buf = None
+
+    def read_into(self, buf, n):
+        fb = self.rd.frame_bytes
+        if self._buf is None or len(self._buf) < n * fb:
+            self._buf = np.empty(n * fb, np.uint8)
+        k = self.rd.read_into(self._buf, n)
+        out = np.frombuffer(memoryview(buf).cast("B"), np.uint8)
+        lb = self.luma_bytes
+        for i in range(k):
+            out[i * lb:(i + 1) * lb] = self._buf[i * fb:i * fb + lb]
+        return k
+
+    def close(self):
+        self.rd.close()
+
+
+def siti_stream(rd, batch=120, normalize=False, device=None):
+    """SI/TI of every frame a luma reader yields, with the host read, the H2D
+    copy and the kernel of neighbouring batches overlapped: a reader thread
+    fills pinned buffers, H2D runs on a copy stream into one of three device
+    slots, pp_siti on a compute stream with the previous batch's last frame
+    (still resident in its slot) as the TI halo.  Slot k+1's H2D waits for
+    batch k-1's kernel (the last reader of that slot)."""
+    import queue
+    import threading
+
+    import torch
+
+    from . import ops
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+    B, lb = int(batch), rd.luma_bytes
+    dt = torch.uint16 if rd.depth > 8 else torch.uint8
+    h_in = [torch.empty((B, lb), dtype=torch.uint8).pin_memory() for _ in range(2)]
+    d_in = [torch.empty((B, rd.h, rd.w), dtype=dt, device=dev) for _ in range(3)]
+    copy_s, comp_s = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    comp_done = [None, None, None]
+    free_in, rq, err = queue.Queue(), queue.Queue(maxsize=2), []
+    for i in range(2):
+        free_in.put(i)
+
+    def read_loop():
+        try:
+            while True:
+                slot = free_in.get()
+                n = rd.read_into(h_in[slot].numpy(), B)
+                rq.put((slot, n))
+                if n < B:
+                    return
+        except Exception as e:  # surfaced in the caller's thread
+            err.append(e)
+            rq.put((None, 0))
+
+    th = threading.Thread(target=read_loop, daemon=True)
+    th.start()
+    outs, prev, k = [], None, 0
+    while True:
+        slot, n = rq.get()
+        if slot is None or n == 0:
+            break
+        ds = k % 3
+        with torch.cuda.stream(copy_s):
+            if comp_done[(k + 1) % 3] is not None:  # batch k-2 read slot ds (k-1 used it as halo: waited below)
+                copy_s.wait_event(comp_done[(k + 1) % 3])
+            if comp_done[ds] is not None:
+                copy_s.wait_event(comp_done[ds])
+            d_in[ds].view(torch.uint8).view(B, lb)[:n].copy_(h_in[slot][:n], non_blocking=True)
+            h2d = torch.cuda.Event()
+            h2d.record(copy_s)
+        comp_s.wait_event(h2d)
+        with torch.cuda.stream(comp_s):
+            si, ti = ops.siti(d_in[ds][:n], rd.depth, prev=prev, stream=comp_s, normalize=normalize)
+            ev = torch.cuda.Event()
+            ev.record(comp_s)
+        comp_done[ds] = ev
+        outs.append((si, ti))
+        prev = d_in[ds][n - 1]
+        h2d.synchronize()  # the pinned buffer is free again
+        free_in.put(slot)
+        k += 1
+        if n < B:
+            break
+    th.join(timeout=5.0)
+    if err:
+        raise err[0]
+    comp_s.synchronize()
+    if not outs:
+        return np.zeros(0), np.zeros(0)
+    return (torch.cat([o[0] for o in outs]).cpu().numpy(), torch.cat([o[1] for o in outs]).cpu().numpy())
+
+
+def siti_scale(bitdepth, normalize):
+    """Factor applied to the raw-code-value SI/TI: 1, or 2^-(bitdepth-8) when normalised."""
+    return 1.0 / (1 << (int(bitdepth) - 8)) if normalize else 1.0
+
+
+def siti_yaml_entry(si, ti, bitdepth=None, normalize=False):
+    """The extra "siti" key of <src>.yaml (spec PP-SITI-1).  ``bitdepth`` and
+    ``scale`` record the SRC's luma depth and the factor applied to the raw
+    code values (1, or 2^-(bitdepth-8) with the 8-bit-scale normalisation),
+    so 8- and 10-bit SRCs can be compared."""
     SI, TI = siti_summary(si, ti)
-    return {"si": SI, "ti": TI, "si_frames": [float(v) for v in si],
-            "ti_frames": [None if math.isnan(v) else float(v) for v in ti],
-            "spec": "PP-SITI-1 (ITU-T P.910 Sobel/frame-difference, valid-region SI, ddof=0)"}
+    e = {"si": SI, "ti": TI, "si_frames": [float(v) for v in si],
+         "ti_frames": [None if math.isnan(v) else float(v) for v in ti],
+         "spec": "PP-SITI-1 (ITU-T P.910 Sobel/frame-difference, valid-region SI, ddof=0)"}
+    if bitdepth is not None:
+        e["bitdepth"] = int(bitdepth)
+        e["scale"] = siti_scale(bitdepth, normalize)
+        e["normalized"] = bool(normalize)
+    return e
 
 
-def analyse_src(videofile, ordernum, with_siti=True, src_info=None, stream_sizes=None, reader=None, siti=None):
+def analyse_src(videofile, ordernum, with_siti=True, src_info=None, stream_sizes=None, reader=None, siti=None,
+                normalize=False, bitdepth=None):
     """util/SRC_analysis.py:120-147 plus an extra "siti" key.
 
     get_src_info / get_stream_size go through ffprobe exactly as the
     reference's (pixpath.probe); the keys the reference writes come out
     byte-identical (tests/test_src_analysis_parity.py).  ``src_info`` /
     ``stream_sizes`` replace those probes, ``reader`` the decode for SI/TI
-    (pixpath.io reader), ``siti`` precomputed (si_frames, ti_frames)."""
+    (pixpath.io reader), ``siti`` precomputed (si_frames, ti_frames) of a
+    ``bitdepth``-bit SRC; ``normalize`` puts SI/TI on the 8-bit scale."""
     import yaml
     from . import probe
     videoinfo = src_info if src_info is not None else probe.get_src_info(videofile)
@@ -121,8 +237,11 @@ def analyse_src(videofile, ordernum, with_siti=True, src_info=None, stream_sizes
     ret = {"md5sum": md5hash, "get_stream_size": {"v": stream_sizes["v"], "a": stream_sizes["a"]},
            "get_src_info": videoinfo}
     if with_siti:
-        si, ti = siti if siti is not None else siti_of_file(videofile, reader=reader)
-        ret["siti"] = siti_yaml_entry(si, ti)
+        if siti is not None:
+            si, ti = siti
+        else:
+            si, ti, bitdepth = siti_of_file(videofile, reader=reader, normalize=normalize, with_depth=True)
+        ret["siti"] = siti_yaml_entry(si, ti, bitdepth, normalize)
     yaml_path = videofile + ".yaml"
     with open(yaml_path, "w") as outfile:
         yaml.dump(ret, outfile, default_flow_style=False)
@@ -182,8 +301,10 @@ def add_siti_columns(rows, siti_by_file):
     return out
 
 
-def siti_from_yaml(src_file):
-    """(SI, TI) from <src>.yaml written by analyse_src, or None."""
+def siti_from_yaml(src_file, with_depth=False):
+    """(SI, TI) from <src>.yaml written by analyse_src, or None; with_depth:
+    (SI, TI, bitdepth, scale) -- bitdepth None and scale 1.0 for entries
+    written without them."""
     import yaml
     p = src_file + ".yaml"
     if not os.path.isfile(p):
@@ -191,7 +312,11 @@ def siti_from_yaml(src_file):
     with open(p) as f:
         d = yaml.safe_load(f) or {}
     e = d.get("siti")
-    return (float(e["si"]), float(e["ti"])) if e else None
+    if not e:
+        return None
+    if with_depth:
+        return float(e["si"]), float(e["ti"]), e.get("bitdepth"), float(e.get("scale", 1.0))
+    return float(e["si"]), float(e["ti"])
 
 
 def complexity_parse_args(argv=None):
@@ -209,6 +334,9 @@ def complexity_parse_args(argv=None):
     ap.add_argument("-n", "--dry-run", action="store_true", help="Show what would be run instead of running it")
     ap.add_argument("--siti", default="yaml", choices=["yaml", "gpu", "none"],
                     help="si/ti columns: from <src>.yaml (analyse_src), measured on the GPU when absent, or left out")
+    ap.add_argument("--siti-scale", default="native", choices=["native", "8bit"],
+                    help="si/ti in raw code values of each SRC's bit depth, or all on the 8-bit scale "
+                         "(divided by 2^(bitdepth-8))")
     return ap.parse_args(argv)
 
 
@@ -263,15 +391,26 @@ def complexity_main(argv=None):
               "high": df[df["framerate"] > 30]["complexity"].quantile([0.25, 0.5, 0.75])}
     df["complexity_class"] = df.apply(lambda x: classify_complexity(x["complexity"], x["framerate"], quants), axis=1)
     if a.siti != "none":
+        # si, ti plus the SRC's luma bit depth and the factor applied to its raw
+        # code values (1 native; 2^-(bitdepth-8) on the 8-bit scale)
+        norm = a.siti_scale == "8bit"
         vals = {}
         for f in df["file"]:
             src = src_of[f]
-            v = siti_from_yaml(src)
+            v = siti_from_yaml(src, with_depth=True)
+            if v is not None and norm and v[2] is not None and v[3] == 1.0:  # raw YAML values -> 8-bit scale
+                k = siti_scale(v[2], True)
+                v = (v[0] * k, v[1] * k, v[2], k)
+            elif v is not None and not norm and v[2] is not None and v[3] != 1.0:  # normalised YAML -> raw
+                v = (v[0] / v[3], v[1] / v[3], v[2], 1.0)
             if v is None and a.siti == "gpu":
-                v = siti_summary(*siti_of_file(src))
-            vals[f] = v if v is not None else (float("nan"), float("nan"))
+                si_f, ti_f, depth = siti_of_file(src, normalize=norm, with_depth=True)
+                v = siti_summary(si_f, ti_f) + (depth, siti_scale(depth, norm))
+            vals[f] = v if v is not None else (float("nan"), float("nan"), None, float("nan"))
         df["si"] = [vals[f][0] for f in df["file"]]
         df["ti"] = [vals[f][1] for f in df["file"]]
+        df["siti_bitdepth"] = pd.array([vals[f][2] for f in df["file"]], dtype="Int64")
+        df["siti_scale"] = [vals[f][3] for f in df["file"]]
     csv_file = os.path.join(a.tmp_dir, a.output_file)
     log.info("Writing complexity data to " + str(csv_file))
     df.to_csv(csv_file, index=False)

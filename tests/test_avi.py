@@ -40,3 +40,39 @@ def test_round_trip(tmp_path, limit):
     for k in range(n_used):  # each entry points at an ix00 chunk
         off = struct.unpack_from("<Q", data, i + 24 + 16 * k)[0]
         assert data[off:off + 4] == b"ix00"
+
+
+def _two_stream_avi(path, video_first, vpk, apk, extra):
+    """A hand-built AVI with a video (FFV1) and an audio (PCM) stream, as
+    ffmpeg's remux of a GPU-written AVPVS with `-c:a flac/pcm` lays it out."""
+    c = avi._chunk
+    vstrh = b"vids" + b"FFV1" + struct.pack("<IHHIIIIIIiI4h", 0, 0, 0, 0, 1, 60, 0, len(vpk), 0, -1, 0, 0, 0, 64, 32)
+    vstrf = struct.pack("<IiiHH4sIiiII", 40 + len(extra), 64, 32, 1, 24, b"FFV1", 0, 0, 0, 0, 0) + extra
+    astrh = b"auds" + b"\0\0\0\0" + struct.pack("<IHHIIIIIIiI4h", 0, 0, 0, 0, 1, 48000, 0, 0, 0, -1, 4, 0, 0, 0, 0)
+    astrf = struct.pack("<HHIIHH", 1, 2, 48000, 192000, 4, 16)  # WAVEFORMATEX: w/h/fourcc would read garbage
+    vl = c(b"LIST", b"strl" + c(b"strh", vstrh) + c(b"strf", vstrf))
+    al = c(b"LIST", b"strl" + c(b"strh", astrh) + c(b"strf", astrf))
+    vid, aid = (b"00", b"01") if video_first else (b"01", b"00")
+    hdrl = c(b"LIST", b"hdrl" + c(b"avih", b"\0" * 56) + (vl + al if video_first else al + vl))
+    movi = b"movi"
+    for v, a in zip(vpk, apk):
+        movi += c(vid + b"dc", v) + c(aid + b"wb", a)
+    body = b"AVI " + hdrl + c(b"LIST", movi)
+    with open(path, "wb") as f:
+        f.write(b"RIFF" + struct.pack("<I", len(body)) + body)
+
+
+@pytest.mark.parametrize("video_first", [True, False])
+def test_two_stream_avi_takes_the_video_stream(tmp_path, video_first):
+    rng = np.random.default_rng(2)
+    vpk = [rng.integers(0, 256, int(rng.integers(1, 500)), dtype=np.uint8).tobytes() for _ in range(9)]
+    apk = [rng.integers(0, 256, 3200, dtype=np.uint8).tobytes() for _ in range(9)]
+    extra = b"cfgrecord"
+    path = str(tmp_path / "av.avi")
+    _two_stream_avi(path, video_first, vpk, apk, extra)
+    info, got = avi.read_packets(path)
+    assert got == vpk
+    assert (info["w"], info["h"], info["rate"], info["fourcc"], info["extradata"]) == (64, 32, Fraction(60), b"FFV1",
+                                                                                        extra)
+    info2, index = avi.scan(path)
+    assert [s for _, s in index] == [len(p) for p in vpk]

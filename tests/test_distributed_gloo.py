@@ -81,10 +81,13 @@ def test_spawn_local_two_ranks_gather_equals_single_pass(tmp_path):
     WORLD_SIZE/MASTER_*), each takes its PVS share, SI/TI is gathered over gloo
     to rank 0 and equals the single-process result for every PVS."""
     import sys
+
+    import gloo_selftest
     from pixpath import batch
     out = tmp_path / "res.npz"
     env = dict(os.environ, PYTHONPATH=os.pathsep.join(sys.path))
-    rc = batch.spawn_local(2, [sys.executable, "-m", "pixpath.batch", "--selftest", str(out), "6"], env=env)
+    prog = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gloo_selftest.py")
+    rc = batch.spawn_local(2, [sys.executable, prog, str(out), "6"], env=env)
     assert rc == 0
     r = np.load(out)
     assert int(r["world"]) == 2
@@ -92,7 +95,7 @@ def test_spawn_local_two_ranks_gather_equals_single_pass(tmp_path):
     assert sorted(set(r["ranks"].tolist())) == [0, 1]
     assert np.bincount(r["ranks"]).tolist() == [3, 3]
     for i in range(6):
-        si, ti = siti_ref.siti(batch._selftest_frames(i))
+        si, ti = siti_ref.siti(gloo_selftest.frames(i))
         np.testing.assert_array_equal(r["si"][i], si)
         np.testing.assert_array_equal(r["ti"][i][1:], ti[1:])
         assert r["SI"][i] == si.max() and r["TI"][i] == np.nanmax(ti)

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 RTOL_SI = 1e-4
 
 
-def _run(frames, depth, gpu, prev=None):
+def _run(frames, depth, gpu, prev=None, normalize=False):
     import torch
     from pixpath import ops
     dt = torch.uint16 if depth > 8 else torch.uint8
@@ -22,7 +22,7 @@ def _run(frames, depth, gpu, prev=None):
     if prev is not None:
         pt = torch.from_numpy(np.ascontiguousarray(prev.astype(np.uint16 if depth > 8 else np.uint8))).to(gpu)
     assert t.dtype == dt
-    si, ti = ops.siti(t, depth, prev=pt)
+    si, ti = ops.siti(t, depth, prev=pt, normalize=normalize)
     torch.cuda.synchronize()
     return si.cpu().numpy(), ti.cpu().numpy()
 
@@ -136,3 +136,49 @@ def test_siti_padded_pitch(gpu, depth, w):
     rsi, rti = siti_ref.siti(frames)
     np.testing.assert_allclose(si.cpu().numpy(), rsi, rtol=RTOL_SI, atol=1e-9)
     np.testing.assert_allclose(ti.cpu().numpy()[1:], rti[1:], rtol=1e-12, atol=1e-12)
+
+
+def test_siti_normalize_8bit_equals_shifted_10bit(gpu):
+    """KAT of PP_SITI_NORMALIZE: an 8-bit clip and the same
+    clip << 2 at 10 bits give equal SI/TI on the 8-bit scale (a power-of-two
+    scaling: exact), and the 10-bit raw values are 4x the 8-bit ones."""
+    rng = np.random.default_rng(88)
+    f8 = np.stack([synth.smooth_frame(t, po.YUV420P, 1920, 1080)[0] for t in range(3)] +
+                  [synth.noise_frame(rng, po.YUV420P, 1920, 1080)[0]])
+    f10 = f8.astype(np.uint16) << 2
+    si8, ti8 = _run(f8, 8, gpu, normalize=True)
+    si10, ti10 = _run(f10, 10, gpu, normalize=True)
+    np.testing.assert_array_equal(si8, si10)
+    np.testing.assert_array_equal(ti8[1:], ti10[1:])
+    raw10, rawt10 = _run(f10, 10, gpu)
+    np.testing.assert_array_equal(raw10, 4 * si8)
+    np.testing.assert_array_equal(rawt10[1:], 4 * ti8[1:])
+    rsi, rti = siti_ref.siti(f10, bitdepth=10, normalize=True)
+    np.testing.assert_allclose(si10, rsi, rtol=RTOL_SI)
+    np.testing.assert_allclose(ti10[1:], rti[1:], rtol=1e-12)
+
+
+@pytest.mark.parametrize("fmt_name,batch", [("yuv422p10le", 16), ("yuv420p", 7)])
+def test_siti_of_file_streamed_luma_only(gpu, tmp_path, fmt_name, batch):
+    """SRC-analysis path: a Y4M read luma-only (chroma skipped) through the
+    pinned double-buffered stream, batches smaller than the clip so the TI
+    halo crosses batch boundaries; equals the numpy reference per frame."""
+    from pixpath import io as pio, siti
+    fmt = {"yuv422p10le": po.YUV422P10LE, "yuv420p": po.YUV420P}[fmt_name]
+    n, w, h = 40, 640, 360
+    frames = [synth.smooth_frame(t, fmt, w, h) for t in range(n)]
+    path = str(tmp_path / "src.y4m")
+    wr = pio.Y4MWriter(path, fmt_name, w, h, 60)
+    for f in frames:
+        wr.write(pio.join_planes(synth.batch([f])))
+    wr.close()
+    luma = np.stack([f[0] for f in frames])
+    depth = 10 if "10" in fmt_name else 8
+    si, ti, d = siti.siti_of_file(path, batch=batch, with_depth=True)
+    assert d == depth and len(si) == n
+    rsi, rti = siti_ref.siti(luma)
+    np.testing.assert_allclose(si, rsi, rtol=RTOL_SI, atol=1e-9)
+    assert np.isnan(ti[0])
+    np.testing.assert_allclose(ti[1:], rti[1:], rtol=1e-12, atol=1e-12)
+    sin, tin = siti.siti_of_file(path, batch=batch, normalize=True)
+    np.testing.assert_array_equal(sin, si / (1 << (depth - 8)))

@@ -6,7 +6,8 @@ lib/ffmpeg.get_segment_info, util/complexity_classification.main) on the
 synthetic files of tests/golden/src_scenarios.py with tests/golden/fake_ffprobe.py
 as `ffprobe`.  pixpath runs on the same files with the same fake ffprobe and
 must reproduce the reference byte for byte; the SI/TI additions are the only
-difference (an extra `siti` YAML key, extra `si`, `ti` CSV columns)."""
+difference (an extra `siti` YAML key, extra `si`, `ti`, `siti_bitdepth`,
+`siti_scale` CSV columns)."""
 import contextlib
 import io
 import json
@@ -72,6 +73,10 @@ def test_analyse_src_with_siti_adds_only_the_siti_key(fake_root, name):
     d = yaml.safe_load(text)
     assert d["siti"]["si"] == 11.25 and d["siti"]["ti"] == 4.0
     assert d["siti"]["ti_frames"][0] is None and d["siti"]["si_frames"] == [10.5, 11.25, 9.0]
+    with contextlib.redirect_stdout(io.StringIO()):
+        yp = siti.analyse_src(os.path.join(fake_root, name), ref["ordernum"], siti=(si, ti), bitdepth=10)
+    d = yaml.safe_load(open(yp))
+    assert d["siti"]["bitdepth"] == 10 and d["siti"]["scale"] == 1.0 and d["siti"]["normalized"] is False
 
 
 def test_r_frame_rate_truncates_like_the_reference(fake_root):
@@ -104,25 +109,36 @@ def test_complexity_csv_identical_plus_siti_columns(fake_root):
     import pandas as pd
     from pixpath import siti
     # two SRCs already carry analyse_src YAMLs with SI/TI, the rest have none
-    for name, (s_, t_) in (("SRC101.avi", (61.5, 20.25)), ("SRC104.avi", (40.0, 9.5))):
+    # (SRC104's entry carries its bit depth: 10-bit raw code values)
+    for name, e in (("SRC101.avi", {"si": 61.5, "ti": 20.25}),
+                    ("SRC104.avi", {"si": 40.0, "ti": 9.5, "bitdepth": 10, "scale": 1.0})):
         with open(os.path.join(fake_root, name + ".yaml"), "w") as f:
-            yaml.dump({"md5sum": "-", "siti": {"si": s_, "ti": t_}}, f)
+            yaml.dump({"md5sum": "-", "siti": e}, f)
     argv = ["-i"] + [os.path.join(fake_root, f) for f in sc.COMPLEXITY_INPUTS] + \
         ["-t", os.path.join(fake_root, "complexity"), "-o", "complexity.csv"]
     csv = siti.complexity_main(argv)
     got = pd.read_csv(csv, float_precision="round_trip")
-    assert list(got.columns[-2:]) == ["si", "ti"]
+    extra = ["si", "ti", "siti_bitdepth", "siti_scale"]
+    assert list(got.columns[-4:]) == extra
     ref_text = FX["complexity_csv"]
-    assert got.drop(columns=["si", "ti"]).to_csv(index=False) == ref_text
+    assert got.drop(columns=extra).to_csv(index=False) == ref_text
     # the exact text: every line is the reference's line plus ",si,ti"
     lines = open(csv).read().splitlines()
     ref_lines = ref_text.splitlines()
-    assert lines[0] == ref_lines[0] + ",si,ti"
+    assert lines[0] == ref_lines[0] + ",si,ti,siti_bitdepth,siti_scale"
     for a, b in zip(lines[1:], ref_lines[1:]):
         assert a.startswith(b + ",")
     row = got.set_index("file")
     assert row.loc["SRC101_crf23.avi", "si"] == 61.5 and row.loc["SRC104_crf23.avi", "ti"] == 9.5
     assert np.isnan(row.loc["SRC102_crf23.avi", "si"])
+    assert row.loc["SRC104_crf23.avi", "siti_bitdepth"] == 10 and row.loc["SRC104_crf23.avi", "siti_scale"] == 1.0
+    assert np.isnan(row.loc["SRC101_crf23.avi", "siti_bitdepth"])
+    # the 8-bit scale: SRC104's 10-bit raw values divided by 4, recorded as such
+    csv8 = siti.complexity_main(argv + ["--siti-scale", "8bit", "-o", "c8.csv"])
+    r8 = pd.read_csv(csv8, float_precision="round_trip").set_index("file")
+    assert r8.loc["SRC104_crf23.avi", "si"] == 10.0 and r8.loc["SRC104_crf23.avi", "ti"] == 2.375
+    assert r8.loc["SRC104_crf23.avi", "siti_scale"] == 0.25
+    assert r8.loc["SRC101_crf23.avi", "si"] == 61.5  # depth unknown: left as written
     csv2 = siti.complexity_main(argv + ["--siti", "none", "-o", "plain.csv"])
     assert open(csv2).read() == ref_text
 
