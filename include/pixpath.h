@@ -276,6 +276,8 @@ int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extradata, int extradata_
                            int max_frames, pp_ffv1_dec **out);
 int pp_ffv1_decoder_destroy(pp_ffv1_dec *dec);
 int pp_ffv1_decoder_format(const pp_ffv1_dec *dec);
+/* The slice grid of the stream (configuration record num_h/v_slices). */
+int pp_ffv1_decoder_slices(const pp_ffv1_dec *dec, int *slices_h, int *slices_v);
 int pp_ffv1_decode(pp_ffv1_dec *dec, const uint8_t *packets, const int64_t *frame_sizes, int nframes,
                    const pp_frames *dst, void *stream);
 

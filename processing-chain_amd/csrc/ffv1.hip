@@ -9,16 +9,31 @@
 // GPU shape: the range coder of a slice is one serial dependency chain (each
 // binary decision updates `low/range` and an adaptive state byte), so the
 // unit of parallelism is the slice: ONE LANE PER SLICE, every slice of every
-// frame of the batch at once (600 frames x 16 slices = 9600 lanes).  A lane
-// walks its slice's Y, Cb, Cr samples in raster order: context from
-// (L - TL, TL - T, T - TR), median prediction, residual folded to the bit
-// depth, then put_symbol's binary decisions through its own context states
-// (2 sets x 666 x 32 B in HBM, primed to 128 by a memset; hot contexts stay in
-// L1/L2) and the state-transition tables in LDS.  Bytes go to a per-slice
-// output region with a running CRC-32 (LDS table); ffv1_pack_kernel then lays
-// the slices out as frame packets with their 8-byte footers.
-// Latency-bound by construction (dependent state loads), not HBM-bound: the
-// figure of merit is frames/s against the CPU restatement (bench --workload ffv1).
+// frame of the batch at once (600 frames x 64 slices = 38,400 lanes).  Only
+// the coder itself is serial, so the encode is split in four launches:
+//   ffv1_model_kernel   data-parallel, one thread per slice-plane row: the
+//                       context (quantised L-TL, TL-T, T-TR) and the folded
+//                       median-prediction residual of every sample, as one
+//                       32-bit token, laid out [wave group][sample][lane] so
+//                       the coder's 64 lanes read one coalesced 256-B line per
+//                       sample;
+//   ffv1_code_kernel    one lane per slice: put_symbol on the token stream.  The
+//                       32 state bytes of the current context live in 8 VGPRs;
+//                       the tokens are known in advance, so the state block of
+//                       the sample two steps ahead is loaded while this one is
+//                       coded (forwarded from registers when one of the two
+//                       samples before it uses the same context).  A symbol's
+//                       state bytes are all read before its first decision and
+//                       written back after the last, so the LDS state-table
+//                       lookups never sit on the range-coder chain.  The
+//                       renormalisation only records `low >> 8` (+ one bit)
+//                       per output byte: FFmpeg's outstanding-byte / carry
+//                       logic is deferred to
+//   ffv1_resolve_kernel one lane per slice: renorm_encoder's byte machine over
+//                       those values -> the slice bytes and their CRC-32;
+//   ffv1_pack_kernel    frame packets with their 8-byte slice footers.
+// The coder is latency/issue-bound (dependent range updates, scattered state
+// blocks), not HBM-bound: the figure of merit is frames/s (bench --workload ffv1).
 #include <algorithm>
 #include <cstring>
 #include <memory>
@@ -31,8 +46,7 @@ namespace pp {
 
 constexpr int kFfv1Ctx = 666;   // (11^3 + 1) / 2 contexts per plane set
 constexpr int kCtxSize = 32;    // state bytes per context
-constexpr int kStateBytes = 2 * kFfv1Ctx * kCtxSize + 64;  // + slice-header states, keyframe and end bits
-constexpr int kSlotStride = 40;  // LDS bytes per lane for the cached context
+constexpr int kStateBytes = 2 * kFfv1Ctx * kCtxSize;  // luma and chroma context sets of one slice
 
 // ---- host range coder (configuration record) and state tables -------------
 struct HostRC {
@@ -143,12 +157,17 @@ struct Ffv1Args {
     const uint8_t *src[3];
     int64_t ls[3], fs[3];
     int w, h, bytes, bits, hsub, vsub, nh, nv, nslices;  // nslices = frames * nh * nv
-    uint8_t *out;           // [nslices][cap]
+    uint8_t *out;           // [nslices][cap] slice bytes (ffv1_resolve_kernel)
     int64_t cap;
     uint8_t *states;        // [nslices][kStateBytes], primed to 128
     int64_t *sizes;         // [nslices] coded bytes, -1 = overflow
     uint32_t *crcs;         // [nslices] CRC-32 of the coded bytes
     const uint8_t *tables;  // zero[256], one[256], crc table (1 KB)
+    uint32_t *tok;          // [nslices / 64][tok_len][64] tokens
+    int64_t tok_len;        // tokens per slice, max over the grid
+    uint32_t *raw;          // [nslices][raw_cap] renorm records, two per dword
+    int64_t raw_cap;        // dwords per slice
+    int32_t *nraw;          // [nslices] records, -1 = overflow
 };
 
 __device__ inline int dquant(int d) {  // d already & 0xFF
@@ -227,157 +246,327 @@ struct DevRC {
     }
 };
 
-template <typename T>
-__device__ inline int ldpx(const uint8_t *row, int x) {
-    return reinterpret_cast<const T *>(row)[x];
+// ---- slice geometry (RFC 9043 4.6: slice_x .. in units of the grid) ---------
+struct SliceGeo {
+    int frame, s, sx, sy, x0, x1, y0, y1, lw, lh, cw, ch;
+    __device__ __host__ int len() const { return lw * lh + 2 * cw * ch; }
+};
+__device__ __host__ inline SliceGeo slice_geo(int g, int w, int h, int nh, int nv, int hsub, int vsub) {
+    SliceGeo q;
+    const int per = nh * nv;
+    q.frame = g / per;
+    q.s = g - q.frame * per;
+    q.sy = q.s / nh;
+    q.sx = q.s - q.sy * nh;
+    q.x0 = (int)((int64_t)q.sx * w / nh);
+    q.x1 = (int)((int64_t)(q.sx + 1) * w / nh);
+    q.y0 = (int)((int64_t)q.sy * h / nv);
+    q.y1 = (int)((int64_t)(q.sy + 1) * h / nv);
+    q.lw = q.x1 - q.x0;
+    q.lh = q.y1 - q.y0;
+    q.cw = (q.lw + (1 << hsub) - 1) >> hsub;
+    q.ch = (q.lh + (1 << vsub) - 1) >> vsub;
+    return q;
 }
 
-__global__ __launch_bounds__(64) void ffv1_slice_kernel(const Ffv1Args a) {
-    __shared__ uint8_t s_zero[256], s_one[256];
-    __shared__ uint32_t s_crc[256];
-    // the 32 state bytes of the context the lane is coding with, cached in LDS
-    // (stride 40 B: 2-way bank conflicts at most); written back to HBM when the
-    // lane switches context, so put_symbol's ~10 dependent state accesses per
-    // sample are LDS round trips instead of L1/L2 ones
-    __shared__ __align__(16) uint8_t s_ctx[64 * kSlotStride];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-        s_zero[i] = a.tables[i];
-        s_one[i] = a.tables[256 + i];
-        s_crc[i] = reinterpret_cast<const uint32_t *>(a.tables + 512)[i];
-    }
-    __syncthreads();
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+// ---- 1. modelling: tokens (context key << 16 | folded residual) -------------
+// One thread per (slice, plane row); 64 threads = the 64 lanes of one coder
+// wave.  key = plane set * 666 + |context|; the residual is negated with the
+// context (encode_line), folded to the bit depth, stored as int16.
+template <typename ST>
+__global__ __launch_bounds__(64) void ffv1_model_kernel(const Ffv1Args a) {
+    const int lane = threadIdx.x;
+    const int wg = blockIdx.y;
+    const int g = wg * 64 + lane;
     if (g >= a.nslices) return;
-    const int per = a.nh * a.nv;
-    const int frame = g / per, s = g - frame * per;
-    const int sy = s / a.nh, sx = s - sy * a.nh;
-    uint8_t *const st0 = a.states + (int64_t)g * kStateBytes;
-    DevRC c;
-    c.low = 0; c.range = 0xFF00; c.oc = 0; c.ob = -1;
-    c.p = a.out + (int64_t)g * a.cap;
-    c.end = c.p + a.cap;
-    c.crc = 0;
-    c.over = false;
-    c.zero = s_zero; c.one = s_one; c.crc_tab = s_crc;
-    // header: keyframe bit (first slice of a frame), slice header with its own
-    // 32 states -- all in the slice's state block (primed to 128), not in
-    // private memory
-    uint8_t *const hs = st0 + 2 * kFfv1Ctx * kCtxSize;
-    if (s == 0) c.rac(hs + 32, 1);
-    // slice x, y, width - 1, height - 1 (slice units), table set of Y and of
-    // Cb/Cr, picture_structure 3 (progressive), SAR 1:1 (setsar=1/1)
-    for (int i = 0; i < 9; i++) c.symbol(hs, i == 0 ? sx : i == 1 ? sy : i == 6 ? 3 : i >= 7 ? 1 : 0, false);
-
-    const int x0 = (int)((int64_t)sx * a.w / a.nh), x1 = (int)((int64_t)(sx + 1) * a.w / a.nh);
-    const int y0 = (int)((int64_t)sy * a.h / a.nv), y1 = (int)((int64_t)(sy + 1) * a.h / a.nv);
+    const SliceGeo q = slice_geo(g, a.w, a.h, a.nh, a.nv, a.hsub, a.vsub);
+    int r = blockIdx.x, p, off;
+    if (r < q.lh) {
+        p = 0; off = 0;
+    } else if ((r -= q.lh) < q.ch) {
+        p = 1; off = q.lw * q.lh;
+    } else if ((r -= q.ch) < q.ch) {
+        p = 2; off = q.lw * q.lh + q.cw * q.ch;
+    } else {
+        return;
+    }
+    const int y = r;
+    const int pw = p ? q.cw : q.lw;
+    const int px0 = p ? q.x0 >> a.hsub : q.x0, py0 = p ? q.y0 >> a.vsub : q.y0;
+    const uint8_t *src = p == 0 ? a.src[0] : p == 1 ? a.src[1] : a.src[2];
+    const int64_t ls = p == 0 ? a.ls[0] : p == 1 ? a.ls[1] : a.ls[2];
+    const int64_t fs = p == 0 ? a.fs[0] : p == 1 ? a.fs[1] : a.fs[2];
+    const uint8_t *rowb = src + q.frame * fs + (int64_t)(py0 + y) * ls + (int64_t)px0 * sizeof(ST);
+    const ST *row = reinterpret_cast<const ST *>(rowb);
+    const ST *top = reinterpret_cast<const ST *>(rowb - ls);
     const int mask = (1 << a.bits) - 1, half = 1 << (a.bits - 1);
-    uint8_t *const slot = s_ctx + threadIdx.x * kSlotStride;
-    int cur_key = -1;  // (plane set, context) held in `slot`
-    auto switch_ctx = [&](int key) {
-        if (cur_key >= 0) {
-            uint2 *g = reinterpret_cast<uint2 *>(st0 + cur_key * kCtxSize);
-            const uint2 *l = reinterpret_cast<const uint2 *>(slot);
-#pragma unroll
-            for (int i = 0; i < 4; i++) g[i] = l[i];
+    const uint32_t key0 = p ? kFfv1Ctx : 0;
+    uint32_t *out = a.tok + ((int64_t)wg * a.tok_len + off + (int64_t)y * pw) * 64 + lane;
+    // FFmpeg's sample-buffer borders: 0 above the slice, L = T at column 0,
+    // TL at column 0 = first sample two rows up, TR past the last column = T
+    int T = y > 0 ? top[0] : 0;
+    int TL = y > 1 ? reinterpret_cast<const ST *>(rowb - 2 * ls)[0] : 0;
+    int L = T;
+    int TR = pw > 1 ? (y > 0 ? top[1] : 0) : T;
+    for (int x = 0; x < pw; ++x) {
+        const int v = row[x];
+        int ctx = dquant((L - TL) & 0xFF) + 11 * dquant((TL - T) & 0xFF) + 121 * dquant((T - TR) & 0xFF);
+        int diff = v - median3(L, L + T - TL, T);
+        if (ctx < 0) {
+            ctx = -ctx;
+            diff = -diff;
         }
-        const uint2 *g = reinterpret_cast<const uint2 *>(st0 + key * kCtxSize);
-        uint2 *l = reinterpret_cast<uint2 *>(slot);
-        uint2 v[4];
+        diff &= mask;
+        diff = diff >= half ? diff - (mask + 1) : diff;
+        out[(int64_t)x * 64] = ((key0 + (uint32_t)ctx) << 16) | ((uint32_t)diff & 0xFFFFu);
+        const int nTR = x + 2 < pw ? (y > 0 ? top[x + 2] : 0) : TR;
+        L = v;
+        TL = T;
+        T = TR;
+        TR = nTR;
+    }
+}
+
+// ---- 2. coding ---------------------------------------------------------------
+// The range coder of one lane.  renorm records, per output byte,
+// (low >> 8) | ((low & 0xFF) == 0) << 9 in a 16-bit slot (two per dword);
+// ffv1_resolve_kernel turns them into bytes exactly as renorm_encoder does.
+struct Enc {
+    uint32_t low, range, acc, half;
+    uint32_t *out;
+    int n, cap;
+};
+
+__device__ __forceinline__ void enc_renorm(Enc &c) {
+    if (c.range < 0x100u) {
+        const uint32_t raw = (c.low >> 8) | ((c.low & 0xFFu) == 0u ? 0x200u : 0u);
+        c.acc |= raw << c.half;
+        if (c.half) {
+            if (c.n < c.cap) c.out[c.n] = c.acc;
+            ++c.n;
+            c.acc = 0;
+        }
+        c.half ^= 16u;
+        c.low = (c.low & 0xFFu) << 8;
+        c.range <<= 8;
+    }
+}
+
+// one binary decision with state value s; returns the next state (LDS table
+// lookup: zero[] at 0, one[] at 256), which the caller writes back later
+__device__ __forceinline__ uint32_t enc_rac(Enc &c, uint32_t s, uint32_t bit, const uint8_t *tab) {
+    const uint32_t r1 = __umul24(c.range, s) >> 8;
+    const uint32_t rz = c.range - r1;
+    c.low += bit ? rz : 0u;
+    c.range = bit ? r1 : rz;
+    const uint32_t ns = tab[s | (bit << 8)];
+    enc_renorm(c);
+    return ns;
+}
+
+// state byte k of a 32-byte block held in 8 dwords (k a compile-time constant
+// after unrolling: no dynamic register indexing)
+__device__ __forceinline__ uint32_t sget(const uint32_t (&b)[8], int k) { return (b[k >> 2] >> ((k & 3) * 8)) & 0xFFu; }
+__device__ __forceinline__ void sput(uint32_t (&b)[8], int k, uint32_t v) {
+    b[k >> 2] = (b[k >> 2] & ~(0xFFu << ((k & 3) * 8))) | (v << ((k & 3) * 8));
+}
+// runtime index k in 8..23 (the sign state 11 + e)
+__device__ __forceinline__ uint32_t sget_dyn(const uint32_t (&b)[8], int k) {
+    const int w = k >> 2;
+    const uint32_t x = w == 2 ? b[2] : w == 3 ? b[3] : w == 4 ? b[4] : b[5];
+    return (x >> ((k & 3) * 8)) & 0xFFu;
+}
+__device__ __forceinline__ void sput_dyn(uint32_t (&b)[8], int k, uint32_t v) {
+    const int w = k >> 2;
+    const uint32_t sh = (k & 3) * 8, m = ~(0xFFu << sh), nv = v << sh;
+    b[2] = w == 2 ? (b[2] & m) | nv : b[2];
+    b[3] = w == 3 ? (b[3] & m) | nv : b[3];
+    b[4] = w == 4 ? (b[4] & m) | nv : b[4];
+    b[5] = w == 5 ? (b[5] & m) | nv : b[5];
+}
+
+// put_symbol (ffv1enc.c put_symbol_inline) on a register block, |v| < 1024:
+// every state byte the symbol uses is read from `b` before the first
+// decision and the updated bytes are written after the last one.
+template <bool SIGNED>
+__device__ __forceinline__ void enc_symbol(Enc &c, uint32_t (&b)[8], int v, const uint8_t *tab) {
+    const uint32_t a = (uint32_t)(v < 0 ? -v : v);
+    const bool nz = v != 0;
+    const int e = nz ? 31 - __clz(a) : 0;
+    const uint32_t n0 = enc_rac(c, sget(b, 0), nz ? 0u : 1u, tab);
+    uint32_t nu[10], nm[9], nsg = 0;
+    if (nz) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) v[i] = g[i];
+        for (int i = 0; i < 10; ++i)
+            if (i <= e) nu[i] = enc_rac(c, sget(b, 1 + i), i < e ? 1u : 0u, tab);
 #pragma unroll
-        for (int i = 0; i < 4; i++) l[i] = v[i];
-        cur_key = key;
+        for (int i = 8; i >= 0; --i)
+            if (i < e) nm[i] = enc_rac(c, sget(b, 22 + i), (a >> i) & 1u, tab);
+        if constexpr (SIGNED) nsg = enc_rac(c, sget_dyn(b, 11 + e), v < 0 ? 1u : 0u, tab);
+    }
+    sput(b, 0, n0);
+    if (nz) {
+#pragma unroll
+        for (int i = 0; i < 10; ++i)
+            if (i <= e) sput(b, 1 + i, nu[i]);
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+            if (i < e) sput(b, 22 + i, nm[i]);
+        if constexpr (SIGNED) sput_dyn(b, 11 + e, nsg);
+    }
+}
+
+__device__ __forceinline__ void blk_load(uint32_t (&b)[8], const uint8_t *p) {
+    const uint4 x = reinterpret_cast<const uint4 *>(p)[0], y = reinterpret_cast<const uint4 *>(p)[1];
+    b[0] = x.x; b[1] = x.y; b[2] = x.z; b[3] = x.w; b[4] = y.x; b[5] = y.y; b[6] = y.z; b[7] = y.w;
+}
+__device__ __forceinline__ void blk_store(uint8_t *p, const uint32_t (&b)[8]) {
+    reinterpret_cast<uint4 *>(p)[0] = make_uint4(b[0], b[1], b[2], b[3]);
+    reinterpret_cast<uint4 *>(p)[1] = make_uint4(b[4], b[5], b[6], b[7]);
+}
+__device__ __forceinline__ void blk_sel(uint32_t (&d)[8], bool c, const uint32_t (&x)[8], const uint32_t (&y)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = c ? x[i] : y[i];
+}
+
+__global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
+    __shared__ uint8_t s_tab[512];  // zero[256], one[256]
+    for (int i = threadIdx.x; i < 512; i += 64) s_tab[i] = a.tables[i];
+    __syncthreads();
+    const int lane = threadIdx.x;
+    const int g = blockIdx.x * 64 + lane;
+    if (g >= a.nslices) return;
+    const SliceGeo q = slice_geo(g, a.w, a.h, a.nh, a.nv, a.hsub, a.vsub);
+    const int len = q.len();
+    uint8_t *const st0 = a.states + (int64_t)g * kStateBytes;
+    const uint32_t *tp = a.tok + (int64_t)blockIdx.x * a.tok_len * 64 + lane;
+    Enc c;
+    c.low = 0; c.range = 0xFF00; c.acc = 0; c.half = 0;
+    c.out = a.raw + (int64_t)g * a.raw_cap;
+    c.n = 0; c.cap = (int)a.raw_cap;
+    // keyframe bit (first slice of a frame), then the slice header with its own 32 states:
+    // slice x, y, width - 1, height - 1 (slice units), table set of Y and of Cb/Cr,
+    // picture_structure 3 (progressive), SAR 1:1 (setsar=1/1)
+    if (q.s == 0) (void)enc_rac(c, 128, 1, s_tab);
+    {
+        uint32_t hb[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) hb[i] = 0x80808080u;
+        const int hv[9] = {q.sx, q.sy, 0, 0, 0, 0, 3, 1, 1};
+#pragma unroll
+        for (int i = 0; i < 9; ++i) enc_symbol<false>(c, hb, hv[i], s_tab);
+    }
+    // token stream with block forwarding (see the file comment)
+    uint32_t t0 = len > 0 ? tp[0] : 0u, t1 = len > 1 ? tp[64] : 0u, t2 = len > 2 ? tp[128] : 0u,
+             t3 = len > 3 ? tp[192] : 0u;
+    int km2 = -1, km1 = -1;
+    uint32_t cur[8], prev[8], pre0[8], pre1[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cur[i] = prev[i] = 0u;
+    if (len > 0) blk_load(pre0, st0 + (t0 >> 16) * kCtxSize);
+    if (len > 1 && (t1 >> 16) != (t0 >> 16)) blk_load(pre1, st0 + (t1 >> 16) * kCtxSize);
+    auto step = [&](int i, uint32_t (&pre)[8]) {
+        const int k0 = (int)(t0 >> 16);
+        const int v = (int)(int16_t)(t0 & 0xFFFFu);
+        uint32_t b[8];
+        // block of this sample: the previous sample's, the one before, or the prefetched
+        {
+            uint32_t tmp[8];
+            blk_sel(tmp, k0 == km2, prev, pre);
+            blk_sel(b, k0 == km1, cur, tmp);
+        }
+        // prefetch the block of sample i + 2 unless one of samples i, i + 1 forwards it
+        const int k1 = (int)(t1 >> 16), k2 = (int)(t2 >> 16);
+        if (i + 2 < len && k2 != k0 && k2 != k1) blk_load(pre, st0 + k2 * kCtxSize);
+        const uint32_t tn = i + 4 < len ? tp[(int64_t)(i + 4) * 64] : 0u;
+        enc_symbol<true>(c, b, v, s_tab);
+        if (i + 1 < len && k1 != k0) blk_store(st0 + k0 * kCtxSize, b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            prev[j] = cur[j];
+            cur[j] = b[j];
+        }
+        km2 = km1;
+        km1 = k0;
+        t0 = t1; t1 = t2; t2 = t3; t3 = tn;
     };
-    for (int p = 0; p < 3; p++) {
-        const int pw = p ? ((x1 - x0) + (1 << a.hsub) - 1) >> a.hsub : x1 - x0;
-        const int ph = p ? ((y1 - y0) + (1 << a.vsub) - 1) >> a.vsub : y1 - y0;
-        const int px0 = p ? x0 >> a.hsub : x0, py0 = p ? y0 >> a.vsub : y0;
-        // plane fields by selects, not a runtime index into the argument arrays (private memory)
-        const uint8_t *src = p == 0 ? a.src[0] : p == 1 ? a.src[1] : a.src[2];
-        const int64_t ls = p == 0 ? a.ls[0] : p == 1 ? a.ls[1] : a.ls[2];
-        const int64_t fs = p == 0 ? a.fs[0] : p == 1 ? a.fs[1] : a.fs[2];
-        const uint8_t *base = src + frame * fs + (int64_t)py0 * ls + (int64_t)px0 * a.bytes;
-        const int key0 = p ? kFfv1Ctx : 0;
-        for (int y = 0; y < ph; y++) {
-            const uint8_t *row = base + (int64_t)y * ls;
-            const uint8_t *top = row - ls, *top2 = row - 2 * ls;
-            // sliding neighbours (FFmpeg's sample-buffer borders: 0 above the
-            // slice, L = T at column 0, TL = the row above that's first sample,
-            // TR = T past the last column)
-            int T = y > 0 ? (a.bytes == 2 ? ldpx<uint16_t>(top, 0) : ldpx<uint8_t>(top, 0)) : 0;
-            int TL = y > 1 ? (a.bytes == 2 ? ldpx<uint16_t>(top2, 0) : ldpx<uint8_t>(top2, 0)) : 0;
-            int L = T;
-            // samples one column ahead are loaded before the current one is
-            // coded, so their latency hides behind the range coder
-            auto ld = [&](const uint8_t *r, int x) {
-                return a.bytes == 2 ? ldpx<uint16_t>(r, x) : ldpx<uint8_t>(r, x);
-            };
-            // top row two columns ahead (tr1 = TR of the next column), so the
-            // next column's context -- and the HBM state block it needs, when
-            // it differs from the current one -- is known before this column
-            // is coded: the block's load overlaps the range coder
-            int nv = ld(row, 0);
-            int tr0 = pw > 1 ? (y > 0 ? ld(top, 1) : 0) : T;
-            int tr1 = pw > 2 ? (y > 0 ? ld(top, 2) : 0) : tr0;
-            int pre_key = -1;
-            uint2 pre[4];
-            for (int x = 0; x < pw; x++) {
-                const int TR = tr0, v = nv;
-                if (x + 1 < pw) nv = ld(row, x + 1);
-                const int tr2 = x + 3 < pw ? (y > 0 ? ld(top, x + 3) : 0) : tr1;
-                int ctx = dquant((L - TL) & 0xFF) + 11 * dquant((TL - T) & 0xFF) + 121 * dquant((T - TR) & 0xFF);
-                int diff = v - median3(L, L + T - TL, T);
-                if (ctx < 0) {
-                    ctx = -ctx;
-                    diff = -diff;
-                }
-                diff &= mask;
-                diff = diff >= half ? diff - (mask + 1) : diff;
-                const int key = key0 + ctx;
-                if (key != cur_key) {
-                    if (key == pre_key) {  // prefetched: write the old block back, install the new
-                        uint2 *g = reinterpret_cast<uint2 *>(st0 + cur_key * kCtxSize);
-                        uint2 *l = reinterpret_cast<uint2 *>(slot);
-#pragma unroll
-                        for (int i = 0; i < 4; i++) g[i] = l[i];
-#pragma unroll
-                        for (int i = 0; i < 4; i++) l[i] = pre[i];
-                        cur_key = key;
-                    } else {
-                        switch_ctx(key);
-                    }
-                }
-                // next column: L = v, TL = T, T = TR, TR = tr1
-                if (x + 1 < pw) {
-                    int c1 = dquant((v - T) & 0xFF) + 11 * dquant((T - TR) & 0xFF) + 121 * dquant((TR - tr1) & 0xFF);
-                    const int k1 = key0 + (c1 < 0 ? -c1 : c1);
-                    if (k1 != key) {
-                        const uint2 *g = reinterpret_cast<const uint2 *>(st0 + k1 * kCtxSize);
-#pragma unroll
-                        for (int i = 0; i < 4; i++) pre[i] = g[i];
-                        pre_key = k1;
-                    }
-                }
-                c.symbol(slot, diff, true);
-                tr0 = tr1;
-                tr1 = tr2;
-                TL = T;
-                T = TR;
-                L = v;
-            }
+    int i = 0;
+    for (; i + 1 < len; i += 2) {
+        step(i, pre0);
+        step(i + 1, pre1);
+    }
+    if (i < len) step(i, pre0);
+    // closing 0 bit at state 129 (ffv1enc.c encode_frame), ff_rac_terminate's two flushes
+    (void)enc_rac(c, 129, 0, s_tab);
+    c.range = 0xFF;
+    c.low += 0xFF;
+    enc_renorm(c);
+    c.range = 0xFF;
+    enc_renorm(c);
+    const int nraw = 2 * c.n + (c.half ? 1 : 0);
+    if (c.half) {
+        if (c.n < c.cap) c.out[c.n] = c.acc;
+        ++c.n;
+    }
+    a.nraw[g] = c.n > c.cap ? -1 : nraw;
+}
+
+// ---- 3. bytes: renorm_encoder's outstanding-byte machine ----------------------
+__global__ __launch_bounds__(64) void ffv1_resolve_kernel(const Ffv1Args a) {
+    __shared__ uint32_t s_crc[256];
+    for (int i = threadIdx.x; i < 256; i += 64) s_crc[i] = reinterpret_cast<const uint32_t *>(a.tables + 512)[i];
+    __syncthreads();
+    const int g = blockIdx.x * 64 + threadIdx.x;
+    if (g >= a.nslices) return;
+    const int nraw = a.nraw[g];
+    if (nraw < 0) {
+        a.sizes[g] = -1;
+        return;
+    }
+    const uint32_t *raw = a.raw + (int64_t)g * a.raw_cap;
+    uint32_t *dst = reinterpret_cast<uint32_t *>(a.out + (int64_t)g * a.cap);
+    const int64_t capw = a.cap >> 2;
+    int64_t nb = 0;  // bytes emitted
+    uint32_t word = 0, crc = 0;
+    bool over = false;
+    auto emit = [&](uint32_t v) {
+        v &= 0xFFu;
+        crc = (crc << 8) ^ s_crc[(crc >> 24) ^ v];
+        word |= v << ((nb & 3) * 8);
+        if ((nb & 3) == 3) {
+            if ((nb >> 2) < capw) dst[nb >> 2] = word;
+            else over = true;
+            word = 0;
+        }
+        ++nb;
+    };
+    int ob = -1, oc = 0;
+    uint32_t pair = 0;
+    for (int j = 0; j < nraw; ++j) {
+        if (!(j & 1)) pair = raw[j >> 1];
+        const uint32_t r = (j & 1) ? pair >> 16 : pair & 0xFFFFu;
+        const int hi = (int)(r & 0x1FFu);
+        const bool exact = (r >> 9) & 1u;
+        if (ob < 0) {
+            ob = hi;
+        } else if (hi < 0xFF || (hi == 0xFF && exact)) {  // low <= 0xFF00
+            emit((uint32_t)ob);
+            for (; oc; --oc) emit(0xFFu);
+            ob = hi;
+        } else if (hi >= 0x100) {  // low >= 0x10000: carry
+            emit((uint32_t)ob + 1u);
+            for (; oc; --oc) emit(0x00u);
+            ob = hi - 0x100;
+        } else {
+            ++oc;
         }
     }
-    hs[33] = 129;  // the closing 0 bit at state 129 (ffv1enc.c encode_frame)
-    c.rac(hs + 33, 0);
-    c.range = 0xFF;  // ff_rac_terminate: two one-byte flushes
-    c.low += 0xFF;
-    c.renorm();
-    c.range = 0xFF;
-    c.renorm();
-    const int64_t n = c.p - (a.out + (int64_t)g * a.cap);
-    a.sizes[g] = c.over ? -1 : n;
-    a.crcs[g] = c.crc;
+    if (nb & 3) {
+        if ((nb >> 2) < capw) dst[nb >> 2] = word;
+        else over = true;
+    }
+    a.sizes[g] = over || nb + 8 > a.cap ? -1 : nb;
+    a.crcs[g] = crc;
 }
 
 // Frame packets: slice g's bytes at off[g], then its footer: 24-bit size (BE),
@@ -410,9 +599,11 @@ struct pp_ffv1_enc {
     int fmt = 0, w = 0, h = 0, nh = 1, nv = 1, max_frames = 0;
     FmtInfo fi{};
     int64_t cap = 0;           // per-slice output bytes
+    int64_t tok_len = 0, raw_cap = 0, rows_max = 0;
     uint8_t *slices = nullptr, *states = nullptr, *tables = nullptr;
     int64_t *sizes = nullptr, *off = nullptr;
-    uint32_t *crcs = nullptr;
+    uint32_t *crcs = nullptr, *tok = nullptr, *raw = nullptr;
+    int32_t *nraw = nullptr;
     std::vector<uint8_t> extradata;
 };
 
@@ -474,16 +665,32 @@ extern "C" int pp_ffv1_encoder_create(pp_ctx *ctx, int fmt, int w, int h, int sl
     }
     const int per = slices_h * slices_v;
     const int64_t ns = (int64_t)per * max_frames;
-    const int sw = (w + slices_h - 1) / slices_h, sh = (h + slices_v - 1) / slices_v;
+    const int64_t ns64 = (ns + 63) / 64 * 64;
     const int bytes = fi.depth > 8 ? 2 : 1;
-    const int64_t raw = ((int64_t)sw * sh + 2 * (int64_t)((sw + 1) >> fi.hsub) * ((sh + 1) >> fi.vsub)) * bytes;
-    E->cap = ((raw * 3 / 2 + 4096) + 255) & ~int64_t(255);  // worst-case expansion is far below 1.5x
+    // the largest slice of the grid (slices differ by one column / row at most)
+    int64_t len_max = 0, rows = 0;
+    for (int s = 0; s < per; ++s) {
+        const SliceGeo q = slice_geo(s, w, h, slices_h, slices_v, fi.hsub, fi.vsub);
+        len_max = std::max<int64_t>(len_max, q.len());
+        rows = std::max<int64_t>(rows, q.lh + 2 * q.ch);
+    }
+    E->tok_len = len_max;
+    E->rows_max = rows;
+    const int64_t raw = len_max * bytes;
+    // worst case (uniform noise) codes ~1.1x the raw samples; a slice larger
+    // than the 24-bit footer size field (FFmpeg asserts < 1 << 24) is refused
+    E->cap = ((raw * 3 / 2 + 4096) + 255) & ~int64_t(255);
+    E->cap = std::min<int64_t>(E->cap, ((int64_t)1 << 24) - 256);
+    E->raw_cap = E->cap / 2 + 4;  // two renorm records (one per output byte) per dword
     PP_HIP(hipSetDevice(ctx->device));
     PP_HIP(hipMalloc(&E->slices, E->cap * ns));
     PP_HIP(hipMalloc(&E->states, (size_t)kStateBytes * ns));
     PP_HIP(hipMalloc(&E->sizes, sizeof(int64_t) * ns));
     PP_HIP(hipMalloc(&E->off, sizeof(int64_t) * ns));
     PP_HIP(hipMalloc(&E->crcs, sizeof(uint32_t) * ns));
+    PP_HIP(hipMalloc(&E->tok, sizeof(uint32_t) * (size_t)(ns64 * len_max)));
+    PP_HIP(hipMalloc(&E->raw, sizeof(uint32_t) * (size_t)(ns * E->raw_cap)));
+    PP_HIP(hipMalloc(&E->nraw, sizeof(int32_t) * ns));
     PP_HIP(hipMalloc(&E->tables, 512 + 1024));
     uint8_t tab[512 + 1024];
     rac_states(tab, tab + 256);
@@ -496,7 +703,7 @@ extern "C" int pp_ffv1_encoder_create(pp_ctx *ctx, int fmt, int w, int h, int sl
 extern "C" int pp_ffv1_encoder_destroy(pp_ffv1_enc *E) {
     if (!E) return PP_OK;
     for (void *p : {(void *)E->slices, (void *)E->states, (void *)E->sizes, (void *)E->off, (void *)E->crcs,
-                    (void *)E->tables})
+                    (void *)E->tables, (void *)E->tok, (void *)E->raw, (void *)E->nraw})
         if (p) (void)hipFree(p);
     delete E;
     return PP_OK;
@@ -529,8 +736,15 @@ extern "C" int64_t pp_ffv1_encode(pp_ffv1_enc *E, const pp_frames *src, int nfra
     a.hsub = E->fi.hsub; a.vsub = E->fi.vsub; a.nh = E->nh; a.nv = E->nv; a.nslices = ns;
     a.out = E->slices; a.cap = E->cap; a.states = E->states; a.sizes = E->sizes; a.crcs = E->crcs;
     a.tables = E->tables;
+    a.tok = E->tok; a.tok_len = E->tok_len; a.raw = E->raw; a.raw_cap = E->raw_cap; a.nraw = E->nraw;
+    const int nwg = (ns + 63) / 64;
     PP_HIP(hipMemsetAsync(E->states, 128, (size_t)kStateBytes * ns, st));  // every context of every slice: 128
-    hipLaunchKernelGGL(ffv1_slice_kernel, dim3((ns + 63) / 64), dim3(64), 0, st, a);
+    if (a.bytes == 2)
+        hipLaunchKernelGGL(ffv1_model_kernel<uint16_t>, dim3((unsigned)E->rows_max, nwg), dim3(64), 0, st, a);
+    else
+        hipLaunchKernelGGL(ffv1_model_kernel<uint8_t>, dim3((unsigned)E->rows_max, nwg), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(ffv1_code_kernel, dim3(nwg), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(ffv1_resolve_kernel, dim3(nwg), dim3(64), 0, st, a);
     PP_HIP(hipGetLastError());
     std::vector<int64_t> sizes(ns), off(ns);
     PP_HIP(hipMemcpyAsync(sizes.data(), E->sizes, sizeof(int64_t) * ns, hipMemcpyDeviceToHost, st));
@@ -541,6 +755,9 @@ extern "C" int64_t pp_ffv1_encode(pp_ffv1_enc *E, const pp_frames *src, int nfra
         for (int s = 0; s < per; ++s) {
             const int64_t n = sizes[f * per + s];
             if (n < 0) PP_FAIL(PP_ERR_NOMEM, "frame %d slice %d exceeds its %lld-byte buffer", f, s, (long long)E->cap);
+            if (n + 8 >= ((int64_t)1 << 24))  // the footer's 24-bit size field (ffv1enc.c asserts the same)
+                PP_FAIL(PP_ERR_UNSUPPORTED, "frame %d slice %d: %lld bytes exceed the 24-bit slice size", f, s,
+                        (long long)n);
             off[f * per + s] = total + fsz;
             fsz += n + 8;
         }

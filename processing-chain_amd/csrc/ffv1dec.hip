@@ -354,6 +354,13 @@ extern "C" int pp_ffv1_decoder_destroy(pp_ffv1_dec *D) {
 }
 
 // Format of the decoded frames (PP_FMT_*), from the configuration record.
+extern "C" int pp_ffv1_decoder_slices(const pp_ffv1_dec *D, int *slices_h, int *slices_v) {
+    if (!D || !slices_h || !slices_v) PP_FAIL(PP_ERR_INVALID, "null argument");
+    *slices_h = D->nh;
+    *slices_v = D->nv;
+    return PP_OK;
+}
+
 extern "C" int pp_ffv1_decoder_format(const pp_ffv1_dec *D) {
     if (!D) PP_FAIL(PP_ERR_INVALID, "null decoder");
     if (D->bits == 8) return D->vsub ? PP_FMT_YUV420P : PP_FMT_YUV422P;

@@ -25,7 +25,7 @@ def _chunk(fourcc, payload):
 
 class AviWriter:
     def __init__(self, path, w, h, rate, extradata=b"", fourcc=b"FFV1", riff_limit=RIFF_LIMIT):
-        self.fh = open(path, "wb")
+        self.fh = open(path, "wb", buffering=1 << 22)
         self.w, self.h, self.rate = int(w), int(h), Fraction(rate)
         self.extradata, self.fourcc, self.limit = bytes(extradata), fourcc, riff_limit
         self.riffs = []       # per RIFF: [riff_start, movi_start, [(data_offset, size, key)]]
@@ -94,17 +94,22 @@ class AviWriter:
         self.fh.seek(cur)
 
     def write_packet(self, data, key=True):
-        data = bytes(data)
+        """Append one packet (bytes-like; written without an extra copy)."""
+        data = memoryview(data).cast("B")
+        n = len(data)
         start = self.riffs[-1][0]
-        if self.fh.tell() - start + len(data) + 8 + 16 * (len(self.riffs[-1][2]) + 2) > self.limit \
+        if self.fh.tell() - start + n + 8 + 16 * (len(self.riffs[-1][2]) + 2) > self.limit \
                 and self.riffs[-1][2]:
             self._close_movi()
             self._open_movi()
         off = self.fh.tell() + 8
-        self.fh.write(_chunk(b"00dc", data))
-        self.riffs[-1][2].append((off, len(data), key))
+        self.fh.write(b"00dc" + struct.pack("<I", n))
+        self.fh.write(data)
+        if n & 1:
+            self.fh.write(b"\0")
+        self.riffs[-1][2].append((off, n, key))
         self.total += 1
-        self.max_size = max(self.max_size, len(data))
+        self.max_size = max(self.max_size, n)
 
     def close(self):
         self._close_movi()

@@ -39,10 +39,14 @@ def _device():
 
 
 class CountingWriter:
-    """Writer wrapper: caps the frame count (-t), remembers the last frame (canvas repeat)."""
+    """Writer wrapper: caps the frame count (-t), remembers the last frame (canvas repeat).
+    Forwards device batches (``write_device``) when the inner writer takes them."""
 
     def __init__(self, inner, frame_bytes, cap=None):
         self.inner, self.fb, self.cap, self.n, self.last = inner, frame_bytes, cap, 0, None
+        self.last_dev = None
+        if hasattr(inner, "write_device"):
+            self.write_device = self._write_device
 
     def write(self, frames):
         mv = memoryview(frames).cast("B")
@@ -53,7 +57,41 @@ class CountingWriter:
             return
         self.inner.write(mv[:k * self.fb])
         self.last = bytes(mv[(k - 1) * self.fb:k * self.fb])
+        self.last_dev = None
         self.n += k
+
+    def _write_device(self, frames, stream=None, emit=None):
+        import torch
+        counts = list(emit) if emit is not None else [1] * frames.n
+        if self.cap is not None:
+            room = self.cap - self.n
+            for i, c in enumerate(counts):
+                counts[i] = max(0, min(c, room))
+                room -= counts[i]
+        total = sum(counts)
+        if total <= 0:
+            return
+        self.inner.write_device(frames, stream, counts)
+        self.n += total
+        if self.cap is not None:  # keep the last written frame on the device for the canvas repeat
+            k = max(i for i, c in enumerate(counts) if c > 0)
+            with torch.cuda.stream(stream or torch.cuda.current_stream(frames.device)):
+                self.last_dev = frames.storage[k:k + 1].clone()
+            self.last = None
+
+    def pad_to_cap(self):
+        """overlay eof_action=repeat: the canvas keeps its last frame up to the cap."""
+        if self.cap is None or self.n >= self.cap:
+            return
+        if self.last_dev is not None:
+            from .frames import FrameBatch
+            fmt = self.inner.fmt
+            fb = FrameBatch.interleaved(fmt, self.inner.w, self.inner.h, 1, device=self.last_dev.device,
+                                        storage=self.last_dev)
+            self.write_device(fb, None, [self.cap - self.n])
+        elif self.last is not None:
+            while self.n < self.cap:
+                self.write(self.last)
 
     def close(self):
         self.inner.close()
@@ -123,29 +161,38 @@ def cmd_avpvs(args):
         inner = _open_writer(out, target, W, H, rate, args.vopts, args.aopts,
                              None if args.aopts.strip() == "-an" else args.input, args.y)
     stall = None
-    if args.stall_output:
+    if args.stall_output and not args.gpu_ffv1:
         # create_avpvs_short of a PVS with stalls: compose the stalled AVPVS
         # (the bufferer step's output) from the frames this pass writes
         stall = _StallOutput(args.stall_output, target, W, H, rate, args.buffer, args.skipping, args.spinner,
-                             args.black_frame, args.stall_vopts, args.stall_aopts, args.input, True, dev,
-                             gpu_ffv1=args.gpu_ffv1)
+                             args.black_frame, args.stall_vopts, args.stall_aopts, args.input, True, dev)
         inner = _Tee(inner, stall.push, fb)
     wr = CountingWriter(inner, fb, cap)
     emit = _fps_counts(rd.rate, rate) if args.fps else None
     Pipeline(stage, batch=args.batch, device=dev).run(rd, wr, emit=emit)
-    if cap is not None and wr.last is not None:
-        while wr.n < cap:  # overlay eof_action=repeat: the canvas keeps the last frame
-            wr.write(wr.last)
+    wr.pad_to_cap()
     rd.close()
     wr.close()
     if args.gpu_ffv1:
         _mux_audio(out, args.input, args.aopts)
+    stall_aopts = args.stall_aopts
     if stall is not None:
-        import json
         stall.close()
+        stall_aopts = stall.aopts_written
+    elif args.stall_output:
+        # the stalled AVPVS from the FFV1 AVPVS just written, at the packet
+        # level: pass-through frames are copied packets, only stall frames are
+        # composed and encoded (no second decode / encode of the AVPVS)
+        from .ffv1 import stall_avi
+        events = ast.literal_eval(args.buffer)
+        if stall_avi(out, args.stall_output, events, args.skipping, args.spinner, args.black_frame, dev) is None:
+            raise SystemExit("pixpath: %s is not a GPU-FFV1 AVI" % out)
+        stall_aopts = _mux_stall_audio(args.stall_output, out, args.stall_aopts, events, args.skipping, rate)
+    if args.stall_output:
+        import json
         with open(_record_path(args.stall_output), "w") as f:
             json.dump(_stall_record(out, args.buffer, args.skipping, args.spinner, args.black_frame, args.pix_fmt,
-                                    args.stall_vopts, args.stall_aopts), f)
+                                    args.stall_vopts, args.stall_aopts, written_aopts=stall_aopts), f)
     return 0
 
 
@@ -167,8 +214,39 @@ def _mux_audio(video_avi, audio_src, aopts):
     os.remove(tmp)
 
 
+def _mux_stall_audio(video_avi, audio_src, aopts, events, skipping, rate):
+    """The stalled AVPVS's audio (bufferer's `-a pcm_s16le`): the source's
+    audio with each stall's silence inserted (stall_audio_graph), muxed next to
+    the stream-copied FFV1 video.  Returns the audio options actually written:
+    `-an` when there is no audio, no ffmpeg, or -an was asked."""
+    import shutil
+    import subprocess
+    from .stall import stall_audio_graph, stall_times
+    if aopts.strip() == "-an":
+        return "-an"
+    if not shutil.which("ffmpeg"):
+        print("pixpath: no ffmpeg: %s written without audio" % video_avi, file=sys.stderr)
+        return "-an"
+    from . import io as pio  # pragma: no cover - needs ffmpeg
+    ap = pio.audio_params(audio_src)  # pragma: no cover
+    if ap is None:  # pragma: no cover
+        return "-an"
+    graph = None if skipping else stall_audio_graph(stall_times(events, rate), ap[0], ap[1])  # pragma: no cover
+    tmp = video_avi + ".video.avi"  # pragma: no cover
+    os.replace(video_avi, tmp)  # pragma: no cover
+    cmd = ["ffmpeg", "-nostdin", "-v", "error", "-y", "-i", tmp, "-i", audio_src]  # pragma: no cover
+    cmd += (["-filter_complex", graph, "-map", "0:v", "-map", "[aout]"] if graph else
+            ["-map", "0:v", "-map", "1:a"])  # pragma: no cover
+    subprocess.run(cmd + ["-c:v", "copy"] + aopts.split() + [video_avi], check=True)  # pragma: no cover
+    os.remove(tmp)  # pragma: no cover
+    return aopts  # pragma: no cover
+
+
 class _Tee:
-    """Writer that also pushes each written frame into a StallStream pusher."""
+    """Writer that also pushes each written frame into a StallStream pusher.
+    Frames are pushed as views of the written batch; only the batch's last
+    frame -- the one a stall at the start of the next batch shows -- is
+    copied, because the caller reuses the batch buffer."""
 
     def __init__(self, inner, push, frame_bytes):
         self.inner, self.push, self.fb = inner, push, frame_bytes
@@ -176,8 +254,10 @@ class _Tee:
     def write(self, frames):
         self.inner.write(frames)
         mv = np.frombuffer(memoryview(frames).cast("B"), np.uint8)
-        for i in range(len(mv) // self.fb):
-            self.push.push(mv[i * self.fb:(i + 1) * self.fb].copy())
+        n = len(mv) // self.fb
+        for i in range(n):
+            f = mv[i * self.fb:(i + 1) * self.fb]
+            self.push.push(f.copy() if i == n - 1 else f)
 
     def close(self):
         self.inner.close()
@@ -306,6 +386,8 @@ class _StallOutput:
 
     def __init__(self, out, fmt, w, h, rate, buffer, skipping, spinner_path, black_frame, vopts, aopts,
                  audio_input, overwrite, dev, gpu_ffv1=False):
+        """gpu_ffv1: the output is an FFV1 AVI coded on the GPU (a decoded
+        input that is not a GPU-FFV1 AVI); its audio is muxed by close()."""
         import torch
         from . import io as pio, ops, spinner
         from .frames import FrameBatch
@@ -317,18 +399,21 @@ class _StallOutput:
             anim, delays = spinner.load_apng(spinner_path)
             ops.spinner_upload(anim, fmt, device=dev)
         audio_from, graph = None, None
-        if gpu_ffv1:  # FFV1 encoded on the GPU into an AVI (video only, as `avpvs --gpu-ffv1`)
-            from .ffv1 import Ffv1AviWriter
-            aopts = "-an"
-        if aopts.strip() != "-an" and os.path.splitext(out)[1].lower() not in (".y4m", ".raw", ".yuv"):
+        self.out, self.gpu_ffv1, self.events, self.skipping, self.rate = out, gpu_ffv1, events, skipping, rate
+        self.audio_input, self.aopts = audio_input, aopts
+        self.aopts_written = "-an"
+        if not gpu_ffv1 and aopts.strip() != "-an" and \
+                os.path.splitext(out)[1].lower() not in (".y4m", ".raw", ".yuv"):
             ap = pio.audio_params(audio_input)  # pragma: no cover - needs ffprobe
             if ap is not None:
                 audio_from = audio_input
                 if not skipping:
                     graph = stall_audio_graph(stall_times(events, rate), ap[0], ap[1])
-        if gpu_ffv1:
+        if gpu_ffv1:  # FFV1 encoded on the GPU into an AVI; audio muxed on close
+            from .ffv1 import Ffv1AviWriter
             self.wr = Ffv1AviWriter(out, fmt, w, h, rate, device=dev)
         elif audio_from:  # pragma: no cover - needs ffmpeg
+            self.aopts_written = aopts
             self.wr = pio.FFmpegWriter(out, fmt, w, h, rate, vopts, aopts, audio_from=audio_from,
                                        overwrite="-y" if overwrite else "-n", audio_filter=graph)
         else:
@@ -361,6 +446,9 @@ class _StallOutput:
     def close(self):
         n = self.push.close()
         self.wr.close()
+        if self.gpu_ffv1:
+            self.aopts_written = _mux_stall_audio(self.out, self.audio_input, self.aopts, self.events, self.skipping,
+                                                  self.rate)
         return n
 
 
@@ -372,7 +460,7 @@ def formats_frame_bytes(fmt, w, h):
 # Provenance of a stalled AVPVS written by `cli avpvs --stall-output`: the
 # bufferer step (`cli stall`) keeps that output when this record matches its
 # own arguments and the AVPVS it would read is the one the record names.
-def _stall_record(input_path, buffer, skipping, spinner_path, black_frame, pix_fmt, vopts, aopts):
+def _stall_record(input_path, buffer, skipping, spinner_path, black_frame, pix_fmt, vopts, aopts, written_aopts=None):
     st = os.stat(input_path)
     spin = None
     if not skipping:
@@ -380,7 +468,8 @@ def _stall_record(input_path, buffer, skipping, spinner_path, black_frame, pix_f
             spin = hashlib.sha256(f.read()).hexdigest()
     return {"input": os.path.abspath(input_path), "input_size": st.st_size, "input_mtime_ns": st.st_mtime_ns,
             "buffer": buffer, "skipping": bool(skipping), "spinner_sha256": spin, "black_frame": bool(black_frame),
-            "pix_fmt": pix_fmt, "vopts": vopts, "aopts": aopts}
+            "pix_fmt": pix_fmt, "vopts": vopts, "aopts": aopts,
+            "aopts_written": aopts if written_aopts is None else written_aopts}
 
 
 def _record_path(out):
@@ -404,6 +493,7 @@ def cmd_stall(args):
             want = _stall_record(args.input, args.buffer, args.skipping, args.spinner, args.black_frame,
                                  args.pix_fmt, args.vopts, args.aopts)
             have = json.load(open(rec))
+            want["aopts_written"] = have.get("aopts_written")  # what the fused pass could write
         except (OSError, ValueError):
             want, have = None, {}
         if want == have:
@@ -416,15 +506,31 @@ def cmd_stall(args):
     dev = _device()
     torch.cuda.set_device(dev)
     if args.gpu_ffv1:
-        from .ffv1 import Ffv1AviReader
+        from .ffv1 import Ffv1AviReader, stall_avi
+        events = ast.literal_eval(args.buffer)
+        n = stall_avi(args.input, out, events, args.skipping, args.spinner, args.black_frame, dev)
+        if n is not None:  # packet level: copied input packets + encoded stall frames
+            info_rate = Ffv1AviReader(args.input, batch=1, device=dev).rate
+            _mux_stall_audio(out, args.input, args.aopts, events, args.skipping, info_rate)
+            return 0
         rd = Ffv1AviReader(args.input, device=dev)
     else:
         rd = pio.open_reader(args.input)
     so = _StallOutput(out, rd.fmt, rd.w, rd.h, rd.rate, args.buffer, args.skipping, args.spinner, args.black_frame,
                       args.vopts, args.aopts, args.input, args.y, dev, gpu_ffv1=args.gpu_ffv1)
-    buf = np.empty((1, rd.frame_bytes), np.uint8)
-    while rd.read_into(buf, 1) == 1:
-        so.push.push(buf[0].copy())
+    B = max(1, int(args.batch))
+    # the input in batches, two buffers in turn: the pusher references the
+    # frame before a stall, which must survive the next batch's read
+    bufs = [np.empty((B, rd.frame_bytes), np.uint8) for _ in range(2)]
+    j = 0
+    while True:
+        buf = bufs[j & 1]
+        k = rd.read_into(buf, B)
+        for i in range(k):
+            so.push.push(buf[i])
+        j += 1
+        if k < B:
+            break
     rd.close()
     so.close()
     return 0

@@ -9,6 +9,8 @@ Bitstream choices that differ from ffmpeg's encoder and the parity status
 CPU restatement oracle/ffv1_oracle.c decodes it losslessly) are in DESIGN.md.
 """
 import ctypes
+import queue
+import threading
 
 import numpy as np
 import torch
@@ -63,13 +65,25 @@ class Ffv1Encoder:
                                            sizes.ctypes.data_as(ctypes.c_void_p), _stream(src.planes[0], stream)))
         return self._out[:total], sizes
 
+    def encode_host(self, src, stream=None):
+        """(numpy uint8 view of the packets in a pinned host buffer, frame sizes):
+        encode, then one D2H of the packets (valid until the next call)."""
+        buf, sizes = self.encode(src, stream)
+        n = buf.numel()
+        if getattr(self, "_host", None) is None or self._host.numel() < n:
+            self._host = torch.empty(max(n, 1 << 20), dtype=torch.uint8).pin_memory()
+        st = torch.cuda.current_stream(src.device) if stream is None else stream
+        with torch.cuda.stream(st):
+            self._host[:n].copy_(buf, non_blocking=True)
+        st.synchronize()
+        return self._host[:n].numpy(), sizes
+
     def encode_to_host(self, src, stream=None):
         """List of per-frame packets (bytes)."""
-        buf, sizes = self.encode(src, stream)
-        data = buf.cpu().numpy().tobytes()
+        data, sizes = self.encode_host(src, stream)
         out, off = [], 0
         for n in sizes.tolist():
-            out.append(data[off:off + n])
+            out.append(data[off:off + n].tobytes())
             off += n
         return out
 
@@ -89,6 +103,9 @@ class Ffv1Decoder:
         self.handle = h_
         fid = check(lib().pp_ffv1_decoder_format(h_))
         self.fmt = formats.fmt(fid)
+        nh, nv = ctypes.c_int(), ctypes.c_int()
+        check(lib().pp_ffv1_decoder_slices(h_, ctypes.byref(nh), ctypes.byref(nv)))
+        self.slices = (nh.value, nv.value)
 
     def __del__(self):
         if getattr(self, "handle", None):
@@ -118,34 +135,137 @@ class Ffv1Decoder:
 class Ffv1AviWriter:
     """`cli avpvs --gpu-ffv1`: the AVPVS written as FFV1 encoded on the GPU in
     an AVI (pixpath.avi) -- the `-c:v ffv1 ... <pvs>.avi` of lib/ffmpeg.py:993
-    without ffmpeg's encoder.  Takes dense host frames (the pipeline's writer
-    interface), encodes them in batches."""
+    without ffmpeg's encoder.
 
-    def __init__(self, path, fmt, w, h, rate, slices=(8, 8), batch=64, device=None):
+    Frames accumulate in HBM -- straight from the pipeline's device output
+    (``write_device``: no D2H, no re-upload) or from host frames (``write``) --
+    into batches of ``batch`` frames (default 600, a 10 s PVS at 60 fps: the
+    encoder's parallelism is frames x slices).  A full batch is encoded by a
+    worker thread on its own stream while the next batch fills (two staging
+    batches), its packets come back in one pinned D2H and go into the AVI."""
+
+    def __init__(self, path, fmt, w, h, rate, slices=(8, 8), batch=600, device=None):
         from . import avi
         from .frames import FrameBatch
         self.fmt = formats.fmt(fmt)
+        self.w, self.h = int(w), int(h)
         self.fb = formats.frame_bytes(self.fmt, w, h)
         self.batch = int(batch)
         self.enc = Ffv1Encoder(self.fmt, w, h, slices=slices, max_frames=self.batch, device=device)
-        dev = torch.device("cuda", self.enc.ctx.device)
-        self.stage = FrameBatch.interleaved(self.fmt, w, h, self.batch, device=dev)
+        self.device = torch.device("cuda", self.enc.ctx.device)
+        self.stages = [FrameBatch.interleaved(self.fmt, w, h, self.batch, device=self.device) for _ in range(2)]
+        self.free = [threading.Event(), threading.Event()]
+        for e in self.free:
+            e.set()
+        self.cur, self.fill = 0, 0
+        self.free[0].clear()
+        self.stream = torch.cuda.Stream(self.device)
+        self.put_stream = torch.cuda.Stream(self.device)  # host-frame uploads
         self.avi = avi.AviWriter(path, w, h, rate, extradata=self.enc.extradata)
+        self.frames = 0
+        self.last_stream = self.put_stream
+        self.q = queue.Queue()
+        self.err = []
+        self.th = threading.Thread(target=self._work, daemon=True)
+        self.th.start()
+
+    def _work(self):
+        from .frames import FrameBatch
+        while True:
+            item = self.q.get()
+            if item is None:
+                return
+            slot, n, ev = item
+            try:
+                if not self.err:
+                    self.stream.wait_event(ev)
+                    src = FrameBatch.interleaved(self.fmt, self.w, self.h, n, device=self.device,
+                                                 storage=self.stages[slot].storage[:n])
+                    with torch.cuda.stream(self.stream):
+                        data, sizes = self.enc.encode_host(src, stream=self.stream)
+                    off = 0
+                    for k in sizes.tolist():
+                        self.avi.write_packet(data[off:off + k])
+                        off += k
+            except Exception as e:  # surfaced by the next write / close
+                self.err.append(e)
+            finally:
+                self.free[slot].set()
+
+    def _check(self):
+        if self.err:
+            raise self.err[0]
+
+    def _submit(self, stream):
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self.q.put((self.cur, self.fill, ev))
+        self.cur ^= 1
+        self.free[self.cur].wait()
+        self.free[self.cur].clear()
+        self.fill = 0
+        self._check()
+
+    def _put(self, rows, stream):
+        """Append device frames (uint8 rows [k, frame_bytes]) on `stream`."""
+        k, i = rows.shape[0], 0
+        while i < k:
+            take = min(k - i, self.batch - self.fill)
+            with torch.cuda.stream(stream):
+                self.stages[self.cur].storage[self.fill:self.fill + take].copy_(rows[i:i + take], non_blocking=True)
+            self.fill += take
+            self.frames += take
+            i += take
+            self.last_stream = stream
+            if self.fill == self.batch:
+                self._submit(stream)
+        if stream is self.put_stream:  # host uploads complete before any event on another stream
+            stream.synchronize()
+
+    def write_device(self, frames, stream=None, emit=None):
+        """Append a device FrameBatch (interleaved) in order; ``emit[i]``: how
+        many times frame i is written (vf_fps duplicates / drops)."""
+        self._check()
+        stream = stream or torch.cuda.current_stream(self.device)
+        rows = frames.storage[:frames.n]
+        if emit is None:
+            self._put(rows, stream)
+            return
+        i, n = 0, len(emit)
+        while i < n:  # runs of single frames go in one copy
+            j = i
+            while j < n and emit[j] == 1:
+                j += 1
+            if j > i:
+                self._put(rows[i:j], stream)
+                i = j
+                continue
+            for _ in range(emit[i]):
+                self._put(rows[i:i + 1], stream)
+            i += 1
 
     def write(self, frames_u8):
-        from .frames import FrameBatch
+        """Append dense host frames."""
         data = np.frombuffer(memoryview(frames_u8).cast("B"), np.uint8)
         n = len(data) // self.fb
-        for i in range(0, n, self.batch):
-            k = min(self.batch, n - i)
-            self.stage.storage[:k].copy_(torch.from_numpy(data[i * self.fb:(i + k) * self.fb].reshape(k, self.fb)))
-            src = FrameBatch.interleaved(self.fmt, self.enc.w, self.enc.h, k, device=self.stage.device,
-                                         storage=self.stage.storage[:k])
-            for p in self.enc.encode_to_host(src):
-                self.avi.write_packet(p)
+        if n == 0:
+            return
+        with torch.cuda.stream(self.put_stream):
+            d = torch.from_numpy(data[:n * self.fb].reshape(n, self.fb)).to(self.device, non_blocking=False)
+        self._put(d, self.put_stream)
 
     def close(self):
-        self.avi.close()
+        try:
+            if self.fill:
+                ev = torch.cuda.Event()
+                ev.record(self.last_stream)
+                self.q.put((self.cur, self.fill, ev))
+                self.fill = 0
+            self.q.put(None)
+            self.th.join()
+            self._check()
+        finally:
+            self.avi.close()
 
 
 class Ffv1AviReader:
@@ -214,3 +334,69 @@ class Ffv1AviReader:
 
     def close(self):
         self.fh.close()
+
+
+def stall_avi(src_path, dst_path, buffer_events, skipping, spinner_path=None, black_frame=True, device=None):
+    """PP-STALL-1 (the bufferer step, p03_generateAvPvs.py:236-243) on an
+    all-intra FFV1 AVI written by Ffv1AviWriter, at the PACKET level: every
+    output frame that is an input frame (pass-through, or a frozen copy with
+    --skipping) is that frame's packet copied from the input file -- no decode,
+    no encode; only the stall frames (frozen / black frame + spinner) are
+    composed on the GPU, from the few source frames decoded for them, and
+    FFV1-encoded with the input's own configuration.  Returns the output frame
+    count, or None when the input's configuration record is not this
+    encoder's (then the caller decodes and re-encodes every frame)."""
+    from . import avi, ops, spinner, stall
+    from .frames import FrameBatch
+    info, index = avi.scan(src_path)
+    if info.get("fourcc") != b"FFV1":
+        return None
+    rate, w, h = info["rate"], info["w"], info["h"]
+    dec = Ffv1Decoder(info["extradata"], w, h, max_frames=1, device=device)
+    enc_probe = Ffv1Encoder(dec.fmt, w, h, slices=dec.slices, host_only=True)
+    if enc_probe.extradata != info["extradata"]:
+        return None
+    delays = None
+    if not skipping:
+        anim, delays = spinner.load_apng(spinner_path)
+    seq = stall.stall_schedule(buffer_events, rate, len(index), skipping, delays, black_frame)
+    compose = [(s, sp) for s, sp in seq if sp >= 0 or s < 0]
+    dev = torch.device("cuda", dec.ctx.device)
+    packets = []
+    with open(src_path, "rb") as fh:
+        def packet(i):
+            off, size = index[i]
+            fh.seek(off)
+            return fh.read(size)
+        if compose:
+            ops.spinner_upload(anim, dec.fmt, device=dev.index)
+            srcs = sorted({s for s, _ in compose if s >= 0})
+            pos = {s: k for k, s in enumerate(srcs)}
+            sb = FrameBatch.interleaved(dec.fmt, w, h, max(1, len(srcs)), device=dev)
+            for k, s in enumerate(srcs):  # one packet per distinct stall source (the frame before each stall)
+                pk = packet(s)
+                dec.decode(pk, [len(pk)], dst=FrameBatch.interleaved(dec.fmt, w, h, 1, device=dev,
+                                                                      storage=sb.storage[k:k + 1]))
+            B = min(600, len(compose))
+            enc = Ffv1Encoder(dec.fmt, w, h, slices=dec.slices, max_frames=B, device=dev)
+            out = FrameBatch.interleaved(dec.fmt, w, h, B, device=dev)
+            for i in range(0, len(compose), B):
+                part = compose[i:i + B]
+                m = len(part)
+                dst = FrameBatch.interleaved(dec.fmt, w, h, m, device=dev, storage=out.storage[:m])
+                ops.stall_compose(sb, [pos[s] if s >= 0 else -1 for s, _ in part], [sp for _, sp in part], dst=dst)
+                data, sizes = enc.encode_host(dst)
+                o = 0
+                for k in sizes.tolist():
+                    packets.append(data[o:o + k].tobytes())
+                    o += k
+        wr = avi.AviWriter(dst_path, w, h, rate, extradata=info["extradata"])
+        j = 0
+        for s, sp in seq:
+            if sp >= 0 or s < 0:
+                wr.write_packet(packets[j])
+                j += 1
+            else:
+                wr.write_packet(packet(s))
+        wr.close()
+    return len(seq)

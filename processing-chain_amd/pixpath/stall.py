@@ -103,7 +103,10 @@ class StallStream:
     def pusher(self, emit_input, emit_stall):
         """The same walk, frame by frame: ``push(frame)`` for every input frame
         in order, then ``close()`` (returns the input frame count).  Lets the
-        AVPVS writer compose the stalled output while it writes the AVPVS."""
+        AVPVS writer compose the stalled output while it writes the AVPVS.
+        A pushed frame is referenced, not copied: it must stay valid until the
+        next push (or close, for the last one); frames kept longer (freeze
+        spans) are copied here."""
         return _FreezePush(self, emit_input) if self.skipping else _StallPush(self, emit_input, emit_stall)
 
 
@@ -145,7 +148,8 @@ class _FreezePush:
                 owner = a
         for a, _ in self.s.spans:
             if a == self.i and a not in self.held:
-                self.held[a] = self.prev if a > 0 else f
+                h = self.prev if a > 0 else f
+                self.held[a] = h.copy() if hasattr(h, "copy") else h
         self.emit_input(f if owner is None else self.held[owner])
         self.prev, self.i = f, self.i + 1
 

@@ -194,3 +194,82 @@ def test_cli_stall_through_gpu_ffv1(gpu, tmp_path):
         assert r1 == r2 == 0
         for p in range(3):
             np.testing.assert_array_equal(d1[p], d2[p])
+
+
+def _black(fid, w, h):
+    depth, hs, vs = po.fmt_info(fid)
+    dt = np.uint16 if depth > 8 else np.uint8
+    return [np.full(s, (16 if p == 0 else 128) << (depth - 8), dt) for p, s in enumerate(po.plane_shapes(fid, w, h))]
+
+
+@pytest.mark.parametrize("skipping,buf", [(False, "[[0,0.1],[0.3,0.05],[9,0.05]]"), (True, "[[0.1,0.1],[0.25,0.2]]")])
+def test_packet_level_stall_matches_oracle(gpu, tmp_path, skipping, buf):
+    """PP-STALL-1 on a GPU-FFV1 AVPVS at the packet level (ffv1.stall_avi,
+    what `cli stall --gpu-ffv1` and the fused `avpvs --stall-output --gpu-ffv1`
+    run): every output packet decodes (C restatement) to the oracle's frame --
+    the scaled input, the frozen / black frame with the spinner -- and every
+    pass-through frame is the input packet byte for byte."""
+    import ast
+    from pixpath import avi, cli, io as pio, spinner, stall
+    rng = np.random.default_rng(21)
+    n, fid = 30, po.YUV420P
+    frames = [synth.noise_frame(rng, fid, 320, 180) for _ in range(n)]
+    seg, wo, out = (str(tmp_path / x) for x in ("seg.y4m", "wo.avi", "pvs.avi"))
+    wr = pio.Y4MWriter(seg, "yuv420p", 320, 180, 60)
+    wr.write(pio.join_planes(synth.batch(frames)))
+    wr.close()
+    sp_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "spinner-128-white.png")
+    assert cli.main(["avpvs", "-y", "--input", seg, "--size", "640x360", "--pix-fmt", "yuv420p", "--aopts=-an",
+                     "--gpu-ffv1", wo]) == 0
+    args = ["stall", "-y", "--input", wo, "--buffer", buf, "--pix-fmt", "yuv420p", "--spinner", sp_path,
+            "--black-frame", "--aopts=-an", "--gpu-ffv1", out]
+    if skipping:
+        args.insert(-1, "--skipping")
+    assert cli.main(args) == 0
+    iw, pin = avi.read_packets(wo)
+    io_, pout = avi.read_packets(out)
+    assert io_["extradata"] == iw["extradata"]
+    anim, delays = spinner.load_apng(sp_path)
+    seq = stall.stall_schedule(ast.literal_eval(buf), 60, n, skipping, delays, True)
+    assert len(pout) == len(seq)
+    scaled = [po.scale(fid, f, fid, 640, 360, po.SWS_BICUBIC) for f in frames]
+    yuva = {}
+    for k, (s, sp) in enumerate(seq):
+        if sp < 0 and s >= 0:
+            assert pout[k] == pin[s], "pass-through frame %d is not the input packet" % k
+            continue
+        base = scaled[s] if s >= 0 else _black(fid, 640, 360)
+        if sp >= 0:
+            if sp not in yuva:
+                yuva[sp] = po.spinner_to_yuva(anim[sp], fid)
+            base = po.overlay_spinner(fid, base, yuva[sp])
+        rc, dec = ref.decode_frame(io_["extradata"], pout[k], 640, 360, 8, 1, 1)
+        assert rc == 0
+        for p in range(3):
+            np.testing.assert_array_equal(dec[p], base[p], err_msg="output frame %d plane %d" % (k, p))
+
+
+def test_writer_device_batches_and_canvas_repeat(gpu, tmp_path):
+    """create_avpvs_segment through the GPU FFV1 writer fed with device
+    batches (no D2H): the canvas of D*R frames repeats the last scaled frame,
+    every packet decodes to the oracle's two-stage chain output."""
+    from pixpath import avi, cli, io as pio
+    rng = np.random.default_rng(31)
+    frames = [synth.noise_frame(rng, po.YUV422P10LE, 320, 180) for _ in range(50)]
+    seg, out = str(tmp_path / "seg.y4m"), str(tmp_path / "tmp_seg.avi")
+    wr = pio.Y4MWriter(seg, "yuv422p10le", 320, 180, 60)
+    wr.write(pio.join_planes(synth.batch(frames)))
+    wr.close()
+    assert cli.main(["avpvs", "-y", "--input", seg, "--size", "640x360", "--pix-fmt", "yuv422p10le", "--fps", "60",
+                     "--duration", "1", "--overlay-yuv420", "--aopts=-an", "--gpu-ffv1", "--batch", "16", out]) == 0
+    info, pk = avi.read_packets(out)
+    assert len(pk) == 60
+    for k in (0, 17, 49, 50, 59):
+        f = frames[min(k, 49)]
+        mid = po.scale(po.YUV422P10LE, f, po.YUV420P, 640, 360, po.SWS_BICUBIC)
+        want = po.scale(po.YUV420P, mid, po.YUV422P10LE, 640, 360, po.SWS_BICUBIC)
+        rc, dec = ref.decode_frame(info["extradata"], pk[k], 640, 360, 10, 1, 0)
+        assert rc == 0
+        for p in range(3):
+            np.testing.assert_array_equal(dec[p], want[p])
+    assert pk[50] == pk[59] == pk[49]
