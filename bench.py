@@ -81,6 +81,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every thread of the affinity mask")
     ap.add_argument("--cpu-sweep", default="16,64", help="extra thread counts timed (shorter) beside the full width")
     ap.add_argument("--no-siti-file", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     return ap.parse_args()
 
 
@@ -184,6 +185,8 @@ def cpu_baseline(args, wl):
            "host_affinity": aff, "cgroup_cpus": quota, "cpu_model": model,
            "scale_fps": top["scale_fps"], "sweep": sweep,
            "per_thread_scale_fps": round(top["scale_fps"] / top["threads"], 2)}
+    if args.workload == "config2":
+        out["e2e"] = cpu_e2e(top["threads"], wl, sws, outs, po)
     if siti_wh:
         out["siti_fps"] = top["siti_fps"]
         out["sample"] = ("%d-thread oracle C restatement (oracle/pixoracle.c + siti_oracle.c, gcc -O3), the best point "
@@ -198,6 +201,43 @@ def cpu_baseline(args, wl):
                          % (top["threads"], full, top["scale_frames"], sw, sh, sfmt, dw, dh, dfmt, flags,
                             top["scale_s"]))
     return out
+
+
+def cpu_e2e(nt, wl, sws, outs, po, frames_per_thread=2):
+    """CPU counterpart of e2e_avpvs: per frame, the oracle's scaler then the
+    oracle's FFV1 encoder (oracle/ffv1_oracle.c, the same bitstream as the GPU
+    encoder, 8x8 slices) on the compressible content e2e_avpvs uses, on nt
+    threads; decode and file writes excluded (a lower bound on the CPU time)."""
+    import threading
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ffv1_ref
+    sfmt, sw, sh, dfmt, dw, dh, flags, _ = wl
+    sf = po.FMT_BY_NAME[sfmt]
+    rng = np.random.default_rng(77)
+    planes = []
+    for p, (r, c) in enumerate(po.plane_shapes(sf, sw, sh)):
+        yy, xx = np.mgrid[0:r, 0:c]
+        planes.append(np.clip((xx * (p + 1) + yy * 2) % 800 + 100 + rng.integers(-4, 5, (r, c)), 64, 940)
+                      .astype(np.uint16))
+    depth, hs, vs = po.fmt_info(po.FMT_BY_NAME[dfmt])
+    done = [0] * nt
+
+    def work(t):
+        for _ in range(frames_per_thread):
+            sws[t].scale_into(planes, outs[t], 1)
+            ffv1_ref.encode_frame(outs[t], depth, hs, vs, 8, 8)
+            done[t] += 1
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=work, args=(t,)) for t in range(nt)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    dt = time.perf_counter() - t0
+    return {"frames_per_s": round(sum(done) / dt, 2), "threads": nt, "frames": sum(done), "seconds": round(dt, 2),
+            "sample": "%d frames: oracle scale 720p->1080p yuv422p10le %s + oracle FFV1 encode (8x8 slices) per "
+                      "frame, %d threads" % (sum(done), flags, nt)}
 
 
 def siti_file(dev, n=600, w=1920, h=1080):
@@ -271,6 +311,69 @@ def pcie_pipeline(wl, n_frames, dev):
             "frames": n, "batch": 60,
             "note": "host pinned -> H2D (copy stream) -> strip_kernel (compute stream) -> D2H -> host; "
                     "host fill of the pinned input is included, decode/encode are not"}
+
+
+def e2e_avpvs(wl, n_frames, dev):
+    """The product path of `cli avpvs --gpu-ffv1` end to end (SURVEY.md 8d's
+    third row): dense host frames -> pinned batches -> H2D -> strip_kernel ->
+    FFV1 encode of the DEVICE output (no D2H of pixels) -> packets D2H -> AVI
+    bytes written to a file.  Host decode is replaced by a memory reader of
+    compressible synthetic frames (moving gradients + noise: FFV1 codes them
+    at ~4:1, like upscaled video); the rate includes the reader's copies and
+    the file writes.  Never `value`."""
+    import tempfile
+    import numpy as np
+    import torch
+    from pixpath import formats, ops
+    from pixpath.ffv1 import Ffv1AviWriter
+    from pixpath.pipeline import Pipeline, Stage
+    sfmt, sw, sh, dfmt, dw, dh, flags, _ = wl
+    in_fb = frame_bytes(sfmt, sw, sh)
+    rng = np.random.default_rng(77)
+    pool = []
+    for k in range(8):
+        planes = []
+        for p, (r, c) in enumerate(formats.plane_shapes(sfmt, sw, sh)):
+            yy, xx = np.mgrid[0:r, 0:c]
+            v = (xx * (p + 1) + yy * 2 + 5 * k) % 800 + 100 + rng.integers(-4, 5, (r, c))
+            planes.append(np.clip(v, 64, 940).astype(np.uint16).view(np.uint8).reshape(-1))
+        pool.append(np.concatenate(planes))
+
+    class MemReader:
+        def __init__(self):
+            self.i = 0
+
+        def read_into(self, buf, n):
+            k = min(n, n_frames - self.i)
+            b = np.frombuffer(buf, np.uint8).reshape(-1, in_fb)
+            for j in range(k):
+                b[j] = pool[(self.i + j) % len(pool)]
+            self.i += k
+            return k
+
+    sc = ops.Scaler(sfmt, sw, sh, dfmt, dw, dh, flags=flags, device=dev.index)
+    stage = Stage(sfmt, sw, sh, dfmt, dw, dh, lambda s, d, st: sc(s, d, stream=st))
+    pl = Pipeline(stage, batch=60, device=dev.index)
+    d = tempfile.mkdtemp(prefix="pixpath_e2e_")
+    path = os.path.join(d, "PVS.avi")
+    try:
+        for rep in range(2):  # the first pass warms the encoder (allocations, kernel loads)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            wr = Ffv1AviWriter(path, dfmt, dw, dh, 60, slices=(8, 8), batch=n_frames, device=dev.index)
+            n = pl.run(MemReader(), wr)
+            wr.close()
+            dt = time.perf_counter() - t0
+        size = os.path.getsize(path)
+    finally:
+        if os.path.exists(path):
+            os.remove(path)
+        os.rmdir(d)
+    return {"frames_per_s": round(n / dt, 1), "frames": n, "seconds": round(dt, 3), "avi_bytes": size,
+            "compression": round(n * frame_bytes(dfmt, dw, dh) / size, 3),
+            "note": "host frames -> pinned batches of 60 -> H2D -> strip_kernel (720p->1080p yuv422p10le lanczos) "
+                    "-> FFV1 v3 encode on the device output (8x8 slices, one 600-frame batch) -> packets D2H -> "
+                    "AVI file; decode of the SRC bitstream excluded (ffmpeg is absent on the box)"}
 
 
 def make_inputs(wl, n, seed, dev):
@@ -430,6 +533,8 @@ def main():
         out["pcie_pipeline"] = pcie_pipeline(wl, 600, dev)
     if world == 1 and siti_wh and not args.no_siti_file:
         out["siti_file"] = siti_file(dev)
+    if world == 1 and args.workload == "config2" and not args.no_e2e:
+        out["e2e_avpvs"] = e2e_avpvs(wl, 600, dev)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, wl)
     print(json.dumps(out), flush=True)

@@ -427,6 +427,8 @@ struct pp_scale_plan {
     pp::PlaneJob fjob[3]{}; // strip_kernel jobs (fast_hw > 0)
     int fast_hw = 0;        // H window dwords of strip_kernel, 0 = generic kernel only
     size_t fast_lds = 0;
+    int fast_tw = 256;      // strip_kernel strip width = threads per workgroup (256 or 512)
+    int fast_tiles = 0;     // strip_kernel workgroups per frame (all planes)
     // CHAIN (pp_scale_chain_plan_create): this plan is the first stage (-> yuv420p)
     pp_scale_plan *stage2 = nullptr;  // yuv420p -> target at the same size (two-launch path)
     int chain_out = 0;                // target bit depth
@@ -446,9 +448,9 @@ struct HostPlane {
     std::vector<int32_t> vbase, vcoef2;  // V window as even-aligned row pairs
     int vtp = 1;
     int tiles_x = 0, nseg = 0, tw = 0, seg_h = 0, cho = 0, ring = 0, maxnew = 0, S = 0;
-    // strip_kernel layout
-    std::vector<int32_t> hbase4, hcoefw, vrow16;
-    int hw_need = 0, max_base = 0, S_fast = 0;
+    // strip_kernel layout (its own strip width f_tw: column windows f_c0 / f_cn)
+    std::vector<int32_t> hbase4, hcoefw, vrow16, f_c0, f_cn;
+    int hw_need = 0, max_base = 0, S_fast = 0, f_tw = 256, f_tiles_x = 0, f_S = 0;
 };
 
 // Vertical taps regrouped as row pairs starting at an even row (the ring keeps
@@ -582,18 +584,30 @@ int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::
     return -1;
 }
 
+// strip_kernel column windows for its strip width tw (256 or 512)
+void fast_tiling(HostPlane &hp, int sw, int dw, int tw) {
+    std::vector<int32_t> c0 = hp.c0, cn = hp.cn;  // the generic tiling's, kept
+    hp.f_S = col_windows(hp, sw, dw, tw);
+    hp.f_c0.swap(hp.c0);
+    hp.f_cn.swap(hp.cn);
+    hp.c0.swap(c0);
+    hp.cn.swap(cn);
+    hp.f_tw = tw;
+    hp.f_tiles_x = (dw + tw - 1) / tw;
+}
+
 // strip_kernel windows: per 4-column lane group, an 8-B aligned base in the
 // staged row and the dwords that hold every non-zero tap of its 4 outputs.
 void fast_windows(HostPlane &hp, int dw) {
-    const int taps = hp.h.taps;
-    hp.hbase4.assign((size_t)hp.tiles_x * 64, 0);
+    const int taps = hp.h.taps, gpt = hp.f_tw / 4;
+    hp.hbase4.assign((size_t)hp.f_tiles_x * gpt, 0);
     hp.hw_need = 1;
     hp.max_base = 0;
-    for (int tx = 0; tx < hp.tiles_x; ++tx)
-        for (int g = 0; g < 64; ++g) {
+    for (int tx = 0; tx < hp.f_tiles_x; ++tx)
+        for (int g = 0; g < gpt; ++g) {
             int lo = INT32_MAX, end = 0;
             for (int j = 0; j < 4; ++j) {
-                const int x = tx * pp::kTileW + 4 * g + j;
+                const int x = tx * hp.f_tw + 4 * g + j;
                 if (x >= dw) break;
                 const int16_t *c = &hp.h.coef[(size_t)x * taps];
                 for (int k = 0; k < taps; ++k)
@@ -603,29 +617,29 @@ void fast_windows(HostPlane &hp, int dw) {
                     }
             }
             if (lo == INT32_MAX) continue;
-            const int base = (lo - hp.c0[tx]) & ~3;
-            hp.hbase4[(size_t)tx * 64 + g] = base;
-            hp.hw_need = std::max(hp.hw_need, (end - hp.c0[tx] - base + 1) / 2);
+            const int base = (lo - hp.f_c0[tx]) & ~3;
+            hp.hbase4[(size_t)tx * gpt + g] = base;
+            hp.hw_need = std::max(hp.hw_need, (end - hp.f_c0[tx] - base + 1) / 2);
             hp.max_base = std::max(hp.max_base, base);
         }
 }
 
 // Taps of every output re-laid over its lane group's HW dwords (zero elsewhere).
 void fast_coefs(HostPlane &hp, int dw, int HW) {
-    const int taps = hp.h.taps;
-    hp.hcoefw.assign((size_t)hp.tiles_x * 64 * 4 * HW, 0);
+    const int taps = hp.h.taps, gpt = hp.f_tw / 4;
+    hp.hcoefw.assign((size_t)hp.f_tiles_x * gpt * 4 * HW, 0);
     uint16_t *h16 = reinterpret_cast<uint16_t *>(hp.hcoefw.data());
-    for (int tx = 0; tx < hp.tiles_x; ++tx)
-        for (int g = 0; g < 64; ++g)
+    for (int tx = 0; tx < hp.f_tiles_x; ++tx)
+        for (int g = 0; g < gpt; ++g)
             for (int j = 0; j < 4; ++j) {
-                const int x = tx * pp::kTileW + 4 * g + j;
+                const int x = tx * hp.f_tw + 4 * g + j;
                 if (x >= dw) break;
-                const int base = hp.hbase4[(size_t)tx * 64 + g];
+                const int base = hp.hbase4[(size_t)tx * gpt + g];
                 for (int k = 0; k < taps; ++k) {
                     const int16_t c = hp.h.coef[(size_t)x * taps + k];
                     if (!c) continue;
-                    const int s = hp.h.pos[x] + k - hp.c0[tx] - base;  // in [0, 2*HW)
-                    h16[(((size_t)tx * 64 + g) * 4 + j) * HW * 2 + s] = (uint16_t)c;
+                    const int s = hp.h.pos[x] + k - hp.f_c0[tx] - base;  // in [0, 2*HW)
+                    h16[(((size_t)tx * gpt + g) * 4 + j) * HW * 2 + s] = (uint16_t)c;
                 }
             }
     // per output row: window base row, then the V tap pairs padded to 8
@@ -715,30 +729,43 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
         if (plan_tiles(hp[c], src_w, src_h, dst_w, dst_h, &P->lds_bytes, &err, c && one_seg_chroma ? 1 << 20 : 0, cho_max))
             PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
     }
-    // strip_kernel eligibility: 256-column strips, <= 8 V tap pairs, one H window
-    // bucket for both planes, single-pass staging, LDS within the budget
+    // strip_kernel eligibility: the generic tiling fits 256-column strips,
+    // <= 8 V tap pairs, one H window bucket for both planes, single-pass
+    // staging, LDS within the budget.  Strip width: 512 (8 waves) for plain
+    // plans when it fits (twice the budget: the same waves per CU), else 256;
+    // chain and packed plans keep 256.  PIXPATH_STRIP_TW=256|512 overrides
+    // (measurement only).
     {
         const char *force = std::getenv("PIXPATH_SCALE_KERNEL");
-        bool ok = !(force && std::strcmp(force, "generic") == 0);
+        const char *etw = std::getenv("PIXPATH_STRIP_TW");
+        bool ok0 = !(force && std::strcmp(force, "generic") == 0);
         const int CH = si.depth > 8 ? 8 : 16;
-        int need = 1;
-        for (int c = 0; c < 2 && ok; ++c) {
-            ok = hp[c].tw == kTileW && hp[c].vtp <= 8;
-            for (int v : hp[c].cn) ok = ok && (v + CH - 1) / CH <= kThreads;
-            if (!ok) break;
-            fast_windows(hp[c], c ? P->cdw : dw);
-            need = std::max(need, hp[c].hw_need);
-        }
-        const int HW = ok ? hw_bucket(need) : -1;
-        size_t lds = 0;
-        for (int c = 0; c < 2 && HW > 0; ++c) {
-            fast_coefs(hp[c], c ? P->cdw : dw, HW);
-            hp[c].S_fast = std::max(hp[c].S, (hp[c].max_base + 2 * HW + 15) & ~15);
-            lds = std::max(lds, (size_t)hp[c].maxnew * hp[c].S_fast * 2 + (size_t)hp[c].ring * kTileW * 2);
-        }
-        if (HW > 0 && lds <= lds_budget()) {
-            P->fast_hw = HW;
-            P->fast_lds = lds;
+        for (int c = 0; c < 2 && ok0; ++c) ok0 = hp[c].tw == kTileW && hp[c].vtp <= 8;
+        int tw_first = (one_seg_chroma || di.packed) ? 256 : 512;
+        if (etw) tw_first = atoi(etw) == 512 ? 512 : 256;
+        for (int ftw = tw_first; ok0 && ftw >= 256; ftw /= 2) {
+            bool ok = true;
+            int need = 1;
+            for (int c = 0; c < 2 && ok; ++c) {
+                fast_tiling(hp[c], c ? P->csw : sw, c ? P->cdw : dw, ftw);
+                for (int v : hp[c].f_cn) ok = ok && (v + CH - 1) / CH <= ftw;
+                if (!ok) break;
+                fast_windows(hp[c], c ? P->cdw : dw);
+                need = std::max(need, hp[c].hw_need);
+            }
+            const int HW = ok ? hw_bucket(need) : -1;
+            size_t lds = 0;
+            for (int c = 0; c < 2 && HW > 0; ++c) {
+                fast_coefs(hp[c], c ? P->cdw : dw, HW);
+                hp[c].S_fast = std::max(hp[c].f_S, (hp[c].max_base + 2 * HW + 15) & ~15);
+                lds = std::max(lds, (size_t)hp[c].maxnew * hp[c].S_fast * 2 + (size_t)hp[c].ring * ftw * 2);
+            }
+            if (HW > 0 && lds <= lds_budget() * (size_t)(ftw / 256)) {
+                P->fast_hw = HW;
+                P->fast_lds = lds;
+                P->fast_tw = ftw;
+                break;
+            }
         }
     }
 
@@ -758,9 +785,22 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
             base += J.tiles_x * J.tiles_y;
             J.vtp = hp[c].vtp; J.ring = hp[c].ring; J.maxnew = hp[c].maxnew; J.S = hp[c].S;
             J.dither_off = p == 2 ? 3 : 0;
-            P->fjob[p] = J;
-            P->fjob[p].S = hp[c].S_fast;
         }
+        int fbase = 0;
+        for (int p = 0; p < 3; ++p) {  // strip_kernel jobs: its own strip width
+            const int c = p ? 1 : 0;
+            PlaneJob &F = P->fjob[p];
+            F = P->job[p];
+            F.S = hp[c].S_fast;
+            if (P->fast_hw) {
+                F.tiles_x = hp[c].f_tiles_x;
+                F.tw = P->fast_tw;
+                F.twl = P->fast_tw == 512 ? 9 : 8;
+            }
+            F.tile_base = fbase;
+            fbase += F.tiles_x * F.tiles_y;
+        }
+        P->fast_tiles = fbase;
     }
     if (!ctx) {
         *out = P.release();
@@ -773,12 +813,13 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
     for (int c = 0; c < 2; ++c)
         total += sz4(hp[c].h.pos.size()) + sz2(hp[c].h.coef.size()) + sz4(hp[c].vbase.size()) +
                  sz4(hp[c].vcoef2.size()) + 2 * sz4(hp[c].c0.size()) + 2 * sz4(hp[c].lo.size()) +
-                 sz4(hp[c].hbase4.size()) + sz4(hp[c].hcoefw.size()) + sz4(hp[c].vrow16.size());
+                 sz4(hp[c].hbase4.size()) + sz4(hp[c].hcoefw.size()) + sz4(hp[c].vrow16.size()) +
+                 sz4(hp[c].f_c0.size()) + sz4(hp[c].f_cn.size());
     PP_HIP(hipSetDevice(ctx->device));
     PP_HIP(hipMalloc(&P->dev, total));
     std::vector<uint8_t> host(total, 0);
     size_t off = 0;
-    const int32_t *dptr32[2][10] = {};
+    const int32_t *dptr32[2][12] = {};
     const int16_t *dptr16[2][1];
     auto put = [&](const void *src, size_t bytes, size_t padded) {
         std::memcpy(host.data() + off, src, bytes);
@@ -799,6 +840,8 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
             dptr32[c][7] = (const int32_t *)put(hp[c].hbase4.data(), hp[c].hbase4.size() * 4, sz4(hp[c].hbase4.size()));
             dptr32[c][8] = (const int32_t *)put(hp[c].hcoefw.data(), hp[c].hcoefw.size() * 4, sz4(hp[c].hcoefw.size()));
             dptr32[c][9] = (const int32_t *)put(hp[c].vrow16.data(), hp[c].vrow16.size() * 4, sz4(hp[c].vrow16.size()));
+            dptr32[c][10] = (const int32_t *)put(hp[c].f_c0.data(), hp[c].f_c0.size() * 4, sz4(hp[c].f_c0.size()));
+            dptr32[c][11] = (const int32_t *)put(hp[c].f_cn.data(), hp[c].f_cn.size() * 4, sz4(hp[c].f_cn.size()));
         }
     }
     PP_HIP(hipMemcpy(P->dev, host.data(), total, hipMemcpyHostToDevice));
@@ -811,8 +854,12 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
         J.tile_c0 = dptr32[c][2]; J.tile_cn = dptr32[c][3];
         J.chunk_lo = dptr32[c][4]; J.chunk_hi = dptr32[c][5];
         J.hbase4 = dptr32[c][7]; J.hcoefw = dptr32[c][8]; J.vrow16 = dptr32[c][9];
-        P->fjob[p] = J;
-        P->fjob[p].S = hp[c].S_fast;
+        PlaneJob &F = P->fjob[p];
+        F.hpos = J.hpos; F.hcoef = J.hcoef; F.vbase = J.vbase; F.vcoef2 = J.vcoef2;
+        F.chunk_lo = J.chunk_lo; F.chunk_hi = J.chunk_hi;
+        F.hbase4 = J.hbase4; F.hcoefw = J.hcoefw; F.vrow16 = J.vrow16;
+        F.tile_c0 = P->fast_hw ? dptr32[c][10] : J.tile_c0;
+        F.tile_cn = P->fast_hw ? dptr32[c][11] : J.tile_cn;
     }
     *out = P.release();
     return PP_OK;
@@ -922,7 +969,7 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
         }
         ring2 = (ring2 + 1) & ~1;
     }
-    const size_t lds = P->fast_lds + (size_t)ring2 * kTileW * 2;
+    const size_t lds = P->fast_lds + (size_t)ring2 * P->fast_tw * 2;
     if (!ok || lds > 64 * 1024) {
         *out = P.release();
         return PP_OK;
@@ -975,8 +1022,9 @@ extern "C" int pp_scale_plan_stats(const pp_scale_plan *P, int64_t *out, int n) 
     if (P->kind == pp_scale_plan::COPY || P->kind == pp_scale_plan::INTERLEAVE) return 0;
     const bool strip = P->fast_hw > 0;
     const pp::PlaneJob &L = strip ? P->fjob[0] : P->job[0];
-    const int64_t v[] = {(int64_t)(strip ? P->fast_lds : P->lds_bytes), strip ? pp::kStripThreads : pp::kThreads,
-                         P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y, L.cho, L.seg_h, L.vtp,
+    const int64_t v[] = {(int64_t)(strip ? P->fast_lds : P->lds_bytes), strip ? P->fast_tw : pp::kThreads,
+                         strip ? P->fast_tiles : P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y, L.cho,
+                         L.seg_h, L.vtp,
                          P->job[1].vtp, L.S, L.ring, L.maxnew};
     const int k = std::min<int>(n, (int)(sizeof(v) / sizeof(v[0])));
     for (int i = 0; i < k; ++i) out[i] = v[i];
@@ -1025,18 +1073,21 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
     const bool tw256 = P->job[0].tw == kTileW && P->job[1].tw == kTileW && P->job[2].tw == kTileW;
     KernelFn k;
     size_t lds = P->lds_bytes;
+    int tiles = P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y, threads = kThreads;
     if (P->fast_hw && a.vec_src) {
         for (int p = 0; p < 3; ++p) a.pl[p] = P->fjob[p];
         lds = P->fast_lds;
+        tiles = P->fast_tiles;
+        threads = P->fast_tw;
         const int vtm = strip_vtm_bucket(std::max(P->fjob[0].vtp, P->fjob[1].vtp));
-        k = P->si.depth == 8 ? pick_strip_u8(out_depth, P->fast_hw, vtm) : pick_strip_u16(out_depth, P->fast_hw, vtm);
+        k = P->si.depth == 8 ? pick_strip_u8(out_depth, P->fast_hw, vtm, P->fast_tw)
+                             : pick_strip_u16(out_depth, P->fast_hw, vtm, P->fast_tw);
     } else if (P->si.depth == 8) {
         k = out_depth == 8 ? pick_ht<uint8_t, 8>(P->ht, tw256) : pick_ht<uint8_t, 10>(P->ht, tw256);
     } else {
         k = out_depth == 8 ? pick_ht<uint16_t, 8>(P->ht, tw256) : pick_ht<uint16_t, 10>(P->ht, tw256);
     }
     if (!k) PP_FAIL(PP_ERR_UNSUPPORTED, "no kernel for %d taps", P->ht);
-    const int tiles = P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y;
     a.tiles = tiles;
     const int fmax = std::max(1, (1 << 30) / tiles);  // 1-D grid size limit
     for (int f0 = 0; f0 < nframes; f0 += fmax) {
@@ -1046,7 +1097,7 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
             b.src[p] += f0 * a.sfs[p];
             b.dst[p] += f0 * a.dfs[p];
         }
-        hipLaunchKernelGGL(k, dim3(tiles * nf), dim3(kThreads), lds, st, b);
+        hipLaunchKernelGGL(k, dim3(tiles * nf), dim3(threads), lds, st, b);
     }
     PP_HIP(hipGetLastError());
     return PP_OK;
@@ -1077,7 +1128,7 @@ int launch_packed(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, 
     const int vtm = strip_vtm_bucket(std::max(P->fjob[0].vtp, P->fjob[1].vtp));
     KernelFn k = P->si.depth == 8 ? pick_strip_packed_u8(P->fast_hw, vtm) : pick_strip_packed_u16(P->fast_hw, vtm);
     if (!k) PP_FAIL(PP_ERR_UNSUPPORTED, "no packed kernel for window %d", P->fast_hw);
-    const int tiles = P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y;
+    const int tiles = P->fast_tiles;
     a.tiles = tiles;
     const int fmax = std::max(1, (1 << 30) / tiles);
     for (int f0 = 0; f0 < nframes; f0 += fmax) {
@@ -1117,7 +1168,7 @@ int launch_chain(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, i
     KernelFn k = P->si.depth == 8 ? pick_strip_chain_u8(P->chain_out, P->fast_hw, vtm)
                                   : pick_strip_chain_u16(P->chain_out, P->fast_hw, vtm);
     if (!k) PP_FAIL(PP_ERR_UNSUPPORTED, "no chain kernel for window %d", P->fast_hw);
-    const int tiles = P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y;
+    const int tiles = P->fast_tiles;
     a.tiles = tiles;
     const int fmax = std::max(1, (1 << 30) / tiles);
     for (int f0 = 0; f0 < nframes; f0 += fmax) {

@@ -205,8 +205,9 @@ __device__ inline void store_raw16(uint16_t *lds_dst, uint4 v) {
 using KernelFn = void (*)(const ScaleArgs);
 // strip_kernel instances (strip_u16.hip, strip_u8.hip): OUTB 8/10, HW window
 // dwords, VTM = largest V tap-pair count over the planes; nullptr if not built
-KernelFn pick_strip_u16(int outb, int hw, int vtm);
-KernelFn pick_strip_u8(int outb, int hw, int vtm);
+// tw: strip width (= threads) 256 or 512
+KernelFn pick_strip_u16(int outb, int hw, int vtm, int tw);
+KernelFn pick_strip_u8(int outb, int hw, int vtm, int tw);
 // chain plans: first stage to 8 bit, second stage into `out2` (8/10) bits
 KernelFn pick_strip_chain_u16(int out2, int hw, int vtm);
 KernelFn pick_strip_chain_u8(int out2, int hw, int vtm);

@@ -106,8 +106,12 @@ __device__ inline void store4(uint8_t *drow, int xo, const int o[4], bool vec, i
 //     15-bit intermediates = hScale8To15 of the identity H filter), and after
 //     each chunk the second stage's vertical filter (vrow2, chunk2 tables)
 //     emits every output row whose taps are all in the ring.
-template <typename ST, int OUTB, int HW, int VTM, int FUSE = 0>
-__global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
+// TW = strip width = threads: 256 (4 waves, one per row group) or 512 (8 waves:
+// row group wave >> 1, column half wave & 1; same 4 outputs per lane, half the
+// strips, so half the column-halo staging and 1-KB contiguous row stores)
+template <typename ST, int OUTB, int HW, int VTM, int FUSE = 0, int TW = 256>
+__global__ __launch_bounds__(TW, (FUSE >= 8 ? 3 : strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
+    static_assert(TW == 256 || TW == 512, "strip width");
     extern __shared__ __align__(16) uint16_t lds[];
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int frame = L / a.tiles;
@@ -118,25 +122,28 @@ __global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)siz
     const PlaneJob &J = a.pl[p];
     t -= J.tile_base;
     const int seg = t / J.tiles_x, tx = t - seg * J.tiles_x;
-    const int x0 = tx * kTileW, nx = min(kTileW, J.dw - x0);
+    const int x0 = tx * TW, nx = min(TW, J.dw - x0);
     const int c0 = as_kconst<int32_t>(J.tile_c0)[tx], cn = as_kconst<int32_t>(J.tile_cn)[tx];
     // chunk tables through the scalar cache: no vector-memory wait at chunk starts
     const kconst int32_t *chunk_lo = as_kconst<int32_t>(J.chunk_lo), *chunk_hi = as_kconst<int32_t>(J.chunk_hi);
     const int S = J.S;
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // row group (H-pass row pairs and V-pass rows strided by 4); at TW = 512
+    // waves 2r and 2r+1 are row group r, left and right 256 columns
+    const int rg = TW == 512 ? wave >> 1 : wave;
     const int lane = tid & 63;
-    const int cx = lane * 4;
+    const int cx = (tid & (TW / 4 - 1)) * 4;
     uint16_t *src_t = lds;                                                  // [maxnew][S]
-    uint32_t *win = reinterpret_cast<uint32_t *>(lds + J.maxnew * S);       // [ring/2][256] row pairs
-    uint32_t *ring2 = win + (J.ring >> 1) * kTileW;                         // FUSE, fuse 2: [ring2/2][256]
+    uint32_t *win = reinterpret_cast<uint32_t *>(lds + J.maxnew * S);       // [ring/2][TW] row pairs
+    uint32_t *ring2 = win + (J.ring >> 1) * TW;                             // FUSE, fuse 2: [ring2/2][TW]
     const kconst int32_t *chunk2 = as_kconst<int32_t>(J.chunk2);            // [nch][4]: lo2, hi2, base2, keep2
     const ST *sbase = reinterpret_cast<const ST *>(a.src[p] + frame * a.sfs[p]);
     uint8_t *dbase = a.dst[p] + frame * a.dfs[p];
 
     // ---- horizontal taps of this lane's 4 columns over its HW-dword window ----
     constexpr int hshift = sizeof(ST) == 1 ? 7 : 9;
-    const int g = tx * 64 + lane;
+    const int g = tx * (TW / 4) + (tid & (TW / 4 - 1));
     const int hb = J.hbase4[g];
     v2i16 hc[4][HW];
     {
@@ -159,13 +166,13 @@ __global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)siz
 
     // ---- staging (16-B loads through the plane's buffer resource) ----------
     constexpr int CH = 16 / sizeof(ST);
-    const int cpr = (cn + CH - 1) / CH;  // 16-B chunks per staged row (<= kThreads, host-checked)
+    const int cpr = (cn + CH - 1) / CH;  // 16-B chunks per staged row (<= TW, host-checked)
     const int64_t sls = a.sls[p];
     const int sw = J.sw;
     const int64_t last_row = std::min<int64_t>(sls, ((int64_t)sw * sizeof(ST) + 15) & ~int64_t(15));
     const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(sbase, (int)((int64_t)(J.sh - 1) * sls + last_row));
     const int cbyte = c0 * (int)sizeof(ST);
-    const int s_rstep = kThreads / cpr;
+    const int s_rstep = TW / cpr;
     const int s_r0 = tid / cpr, s_ch = tid - s_r0 * cpr;
     const bool s_on = s_r0 < s_rstep;
     const int s_lds = s_r0 * S + s_ch * CH;
@@ -245,7 +252,7 @@ __global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)siz
         // lane in increasing order (no lane reads a slot already overwritten)
         bool moved = false;
         if (shift > 0) {
-            for (int k = 0; k < keep; ++k) win[k * kTileW + tid] = win[(k + shift) * kTileW + tid];
+            for (int k = 0; k < keep; ++k) win[k * TW + tid] = win[(k + shift) * TW + tid];
             moved = true;
         }
         int base2 = 0;
@@ -254,7 +261,7 @@ __global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)siz
                 base2 = chunk2[4 * ci + 2];
                 const int shift2 = ci ? (base2 - chunk2[4 * ci - 2]) >> 1 : 0, keep2 = chunk2[4 * ci + 3];
                 if (shift2 > 0) {
-                    for (int k = 0; k < keep2; ++k) ring2[k * kTileW + tid] = ring2[(k + shift2) * kTileW + tid];
+                    for (int k = 0; k < keep2; ++k) ring2[k * TW + tid] = ring2[(k + shift2) * TW + tid];
                     moved = true;
                 }
             }
@@ -266,21 +273,21 @@ __global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)siz
         if (nnew > 0 && !(a.debug & 4)) {
             const int i0 = next_src - base;
             const int kf0 = (i0 + 1) >> 1, kf1 = (i0 + nnew) >> 1;
-            if ((i0 & 1) && wave == ((i0 >> 1) & 3)) {  // high row of a kept pair (same wave moved it)
+            if ((i0 & 1) && rg == ((i0 >> 1) & 3)) {  // high row of a kept pair
                 int o[4];
                 hrow4(src_t, o);
-                uint16_t *w16 = reinterpret_cast<uint16_t *>(win + (i0 >> 1) * kTileW + cx);
+                uint16_t *w16 = reinterpret_cast<uint16_t *>(win + (i0 >> 1) * TW + cx);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) w16[2 * j + 1] = static_cast<uint16_t>(o[j]);
             }
-            if (((i0 + nnew) & 1) && wave == (kf1 & 3)) {  // low row of the last pair
+            if (((i0 + nnew) & 1) && rg == (kf1 & 3)) {  // low row of the last pair
                 int o[4];
                 hrow4(src_t + (nnew - 1) * S, o);
                 uint4 v;
                 v.x = o[0] & 0xffff; v.y = o[1] & 0xffff; v.z = o[2] & 0xffff; v.w = o[3] & 0xffff;
-                *reinterpret_cast<uint4 *>(win + kf1 * kTileW + cx) = v;
+                *reinterpret_cast<uint4 *>(win + kf1 * TW + cx) = v;
             }
-            for (int k = kf0 + wave; k < kf1; k += 4) {
+            for (int k = kf0 + rg; k < kf1; k += 4) {
                 const int ra = 2 * k - i0;
                 int oa[4], ob[4];
                 hrow4(src_t + ra * S, oa);
@@ -290,7 +297,7 @@ __global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)siz
                 v.y = __builtin_amdgcn_perm(ob[1], oa[1], 0x05040100u);
                 v.z = __builtin_amdgcn_perm(ob[2], oa[2], 0x05040100u);
                 v.w = __builtin_amdgcn_perm(ob[3], oa[3], 0x05040100u);
-                *reinterpret_cast<uint4 *>(win + k * kTileW + cx) = v;
+                *reinterpret_cast<uint4 *>(win + k * TW + cx) = v;
             }
             next_src = hi;
         }
@@ -309,7 +316,7 @@ __global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)siz
             // through the scalar cache: one exposed scalar-load latency per
             // group, not per row (the ds_reads of a row depend on its base)
             constexpr int G = VT <= 2 ? 8 : VT <= 5 ? 4 : 2;
-            for (int g0 = wave; g0 < ny; g0 += 4 * G) {
+            for (int g0 = rg; g0 < ny; g0 += 4 * G) {
                 int vb[G];
                 int32_t cf[G][VT];
 #pragma unroll
@@ -326,10 +333,10 @@ __global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)siz
                     if (yy >= ny) break;
                     const int y = y0 + yy;
                     uint8_t *drow_p = dbase + (int64_t)y * dls;
-                    const uint4 *rp = reinterpret_cast<const uint4 *>(win + ((vb[i] - nbase) >> 1) * kTileW + cx);
+                    const uint4 *rp = reinterpret_cast<const uint4 *>(win + ((vb[i] - nbase) >> 1) * TW + cx);
                     uint4 q[VT];
 #pragma unroll
-                    for (int j = 0; j < VT; ++j) q[j] = rp[j * (kTileW / 4)];
+                    for (int j = 0; j < VT; ++j) q[j] = rp[j * (TW / 4)];
                     int acc[4];
                     if constexpr (OUTB == 8) {
                         // ordered dither: the row's 8 bytes (scalar load, y is wave-uniform)
@@ -362,7 +369,7 @@ __global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)siz
                     for (int j = 0; j < 4; ++j) o[j] = min(max(acc[j] >> sh, 0), mx);
                     if constexpr (FUSE >= 8) {
                         if (J.fuse == 2) {  // into ring2 (second-stage input), 15-bit
-                            uint16_t *r16 = reinterpret_cast<uint16_t *>(ring2 + ((y - base2) >> 1) * kTileW + cx);
+                            uint16_t *r16 = reinterpret_cast<uint16_t *>(ring2 + ((y - base2) >> 1) * TW + cx);
 #pragma unroll
                             for (int j = 0; j < 4; ++j) r16[2 * j + (y & 1)] = static_cast<uint16_t>(o[j] << 7);
                             __builtin_amdgcn_sched_barrier(0);
@@ -429,16 +436,16 @@ __global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)siz
                 const int lo2 = chunk2[4 * ci], hi2 = chunk2[4 * ci + 1];
                 const kconst int32_t *vrow2 = as_kconst<int32_t>(J.vrow2);
                 const int vtp2 = J.vtp2;
-                for (int r2 = lo2 + wave; r2 < hi2; r2 += 4) {
+                for (int r2 = lo2 + rg; r2 < hi2; r2 += 4) {
                     const kconst int32_t *row = vrow2 + (int64_t)r2 * 16;
-                    const uint4 *rp = reinterpret_cast<const uint4 *>(ring2 + ((row[0] - base2) >> 1) * kTileW + cx);
+                    const uint4 *rp = reinterpret_cast<const uint4 *>(ring2 + ((row[0] - base2) >> 1) * TW + cx);
                     int acc[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) acc[j] = FUSE == 8 ? 64 << 12 : 1 << (10 + 16 - FUSE);
 #pragma unroll
                     for (int jj = 0; jj < 4; ++jj) {
                         if (jj >= vtp2) break;
-                        const uint4 q = rp[jj * (kTileW / 4)];
+                        const uint4 q = rp[jj * (TW / 4)];
                         const v2i16 c2 = __builtin_bit_cast(v2i16, row[1 + jj]);
                         acc[0] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.x), c2, acc[0], false);
                         acc[1] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.y), c2, acc[1], false);
@@ -461,25 +468,30 @@ __global__ __launch_bounds__(kThreads, (FUSE >= 8 ? 3 : strip_min_waves<(int)siz
 
 inline int strip_vtm_bucket_impl(int vtp) { return vtp <= 2 ? 2 : vtp <= 3 ? 3 : vtp <= 5 ? 5 : 8; }
 
-#define PP_STRIP_VTM(ST, OUTB, HW, FUSE)                                     \
+#define PP_STRIP_VTM(ST, OUTB, HW, FUSE, TW)                                 \
     switch (vtm) {                                                           \
-    case 2: return strip_kernel<ST, OUTB, HW, 2, FUSE>;                      \
-    case 3: return strip_kernel<ST, OUTB, HW, 3, FUSE>;                      \
-    case 5: return strip_kernel<ST, OUTB, HW, 5, FUSE>;                      \
-    default: return strip_kernel<ST, OUTB, HW, 8, FUSE>;                     \
+    case 2: return strip_kernel<ST, OUTB, HW, 2, FUSE, TW>;                  \
+    case 3: return strip_kernel<ST, OUTB, HW, 3, FUSE, TW>;                  \
+    case 5: return strip_kernel<ST, OUTB, HW, 5, FUSE, TW>;                  \
+    default: return strip_kernel<ST, OUTB, HW, 8, FUSE, TW>;                 \
     }
-#define PP_STRIP_HW_F(ST, OUTB, FUSE)                                        \
+#define PP_STRIP_HW_FT(ST, OUTB, FUSE, TW)                                   \
     switch (hw) {                                                            \
-    case 3: PP_STRIP_VTM(ST, OUTB, 3, FUSE)                                  \
-    case 4: PP_STRIP_VTM(ST, OUTB, 4, FUSE)                                  \
-    case 5: PP_STRIP_VTM(ST, OUTB, 5, FUSE)                                  \
-    case 6: PP_STRIP_VTM(ST, OUTB, 6, FUSE)                                  \
-    case 8: PP_STRIP_VTM(ST, OUTB, 8, FUSE)                                  \
-    case 10: PP_STRIP_VTM(ST, OUTB, 10, FUSE)                                \
-    case 12: PP_STRIP_VTM(ST, OUTB, 12, FUSE)                                \
-    case 16: PP_STRIP_VTM(ST, OUTB, 16, FUSE)                                \
+    case 3: PP_STRIP_VTM(ST, OUTB, 3, FUSE, TW)                              \
+    case 4: PP_STRIP_VTM(ST, OUTB, 4, FUSE, TW)                              \
+    case 5: PP_STRIP_VTM(ST, OUTB, 5, FUSE, TW)                              \
+    case 6: PP_STRIP_VTM(ST, OUTB, 6, FUSE, TW)                              \
+    case 8: PP_STRIP_VTM(ST, OUTB, 8, FUSE, TW)                              \
+    case 10: PP_STRIP_VTM(ST, OUTB, 10, FUSE, TW)                            \
+    case 12: PP_STRIP_VTM(ST, OUTB, 12, FUSE, TW)                            \
+    case 16: PP_STRIP_VTM(ST, OUTB, 16, FUSE, TW)                            \
     default: return nullptr;                                                 \
     }
-#define PP_STRIP_HW(ST, OUTB) PP_STRIP_HW_F(ST, OUTB, 0)
+#define PP_STRIP_HW_F(ST, OUTB, FUSE) PP_STRIP_HW_FT(ST, OUTB, FUSE, 256)
+#define PP_STRIP_HW(ST, OUTB)                                                \
+    if (tw == 512) {                                                         \
+        PP_STRIP_HW_FT(ST, OUTB, 0, 512)                                     \
+    }                                                                        \
+    PP_STRIP_HW_FT(ST, OUTB, 0, 256)
 
 }  // namespace pp

@@ -3,7 +3,7 @@
 
 namespace pp {
 
-KernelFn pick_strip_u8(int outb, int hw, int vtm) {
+KernelFn pick_strip_u8(int outb, int hw, int vtm, int tw) {
     if (outb == 8) {
         PP_STRIP_HW(uint8_t, 8)
     }

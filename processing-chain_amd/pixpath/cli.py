@@ -505,19 +505,23 @@ def cmd_stall(args):
         return 0
     dev = _device()
     torch.cuda.set_device(dev)
-    if args.gpu_ffv1:
+    gpu_out = getattr(args, "gpu_ffv1_out", args.gpu_ffv1)
+    if args.gpu_ffv1 and gpu_out:
         from .ffv1 import Ffv1AviReader, stall_avi
         events = ast.literal_eval(args.buffer)
         n = stall_avi(args.input, out, events, args.skipping, args.spinner, args.black_frame, dev)
         if n is not None:  # packet level: copied input packets + encoded stall frames
-            info_rate = Ffv1AviReader(args.input, batch=1, device=dev).rate
-            _mux_stall_audio(out, args.input, args.aopts, events, args.skipping, info_rate)
+            from .avi import scan
+            _mux_stall_audio(out, args.input, args.aopts, events, args.skipping, scan(args.input)[0]["rate"])
             return 0
+        rd = Ffv1AviReader(args.input, device=dev)
+    elif args.gpu_ffv1:
+        from .ffv1 import Ffv1AviReader
         rd = Ffv1AviReader(args.input, device=dev)
     else:
         rd = pio.open_reader(args.input)
     so = _StallOutput(out, rd.fmt, rd.w, rd.h, rd.rate, args.buffer, args.skipping, args.spinner, args.black_frame,
-                      args.vopts, args.aopts, args.input, args.y, dev, gpu_ffv1=args.gpu_ffv1)
+                      args.vopts, args.aopts, args.input, args.y, dev, gpu_ffv1=gpu_out)
     B = max(1, int(args.batch))
     # the input in batches, two buffers in turn: the pusher references the
     # frame before a stall, which must survive the next batch's read
@@ -554,6 +558,10 @@ def cmd_siti(args):
         res["ti_frames"] = [None if np.isnan(v) else float(v) for v in ti]
     print(json.dumps(res))
     return 0
+
+
+def _avi(path):
+    return str(path).lower().endswith(".avi")
 
 
 def main(argv=None):
@@ -631,6 +639,18 @@ def main(argv=None):
     p.set_defaults(fn=cmd_siti)
 
     args = ap.parse_args(argv)
+    # GPU FFV1 applies to AVI files (the reference's AVPVS container); Y4M /
+    # raw files and other containers keep their own readers and writers
+    if getattr(args, "ffv1_input", False):
+        args.ffv1_input = _avi(args.input)
+    if getattr(args, "gpu_ffv1", False):
+        if args.cmd == "avpvs":
+            args.gpu_ffv1 = _avi(args.output)
+        elif args.cmd == "cpvs":
+            args.gpu_ffv1 = _avi(args.input)
+        elif args.cmd == "stall":
+            args.gpu_ffv1 = _avi(args.input)
+            args.gpu_ffv1_out = _avi(args.output)
     return args.fn(args)
 
 

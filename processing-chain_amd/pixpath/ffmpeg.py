@@ -69,11 +69,21 @@ def _skip_existing(output_file, overwrite):
     return "-n", False
 
 
+def ffv1_on_gpu():
+    """The gpu backend's AVPVS codec: FFV1 coded on the GPU into pixpath's own
+    AVI (default), or ffmpeg's FFV1 encoder fed through a
+    pipe with PIXPATH_FFV1=ffmpeg."""
+    v = os.environ.get("PIXPATH_FFV1", "gpu")
+    if v not in ("gpu", "ffmpeg"):
+        raise ValueError("PIXPATH_FFV1 must be 'gpu' or 'ffmpeg'")
+    return v == "gpu"
+
+
 def _gpu_cli(sub, args):
     args = list(args)
-    if os.environ.get("PIXPATH_FFV1") == "gpu":
-        # FFV1 AVPVS coded on the GPU in pixpath's own AVI (opt-in):
-        # the AVPVS writers encode it, its readers (CPVS, stall, mobile scale) decode it
+    if ffv1_on_gpu():
+        # FFV1 AVPVS coded on the GPU in pixpath's own AVI: the AVPVS writers
+        # encode it, its readers (CPVS, stall, mobile scale) decode it there
         if sub == "avpvs" and FFV1_OPTS in args:
             args.insert(-1, "--gpu-ffv1")
         elif sub == "avpvs":

@@ -104,5 +104,7 @@ def test_gpu_ffv1_opt_in_flags(monkeypatch):
     assert pff._gpu_cli("avpvs", ["-y", "--vopts", "-c:v libx264", "/o.mp4"]).endswith("--ffv1-input /o.mp4")
     assert pff._gpu_cli("cpvs", ["-y", "/c.avi"]).endswith("--gpu-ffv1 /c.avi")
     assert pff._gpu_cli("stall", ["-y", "/s.avi"]).endswith("--gpu-ffv1 /s.avi")
-    monkeypatch.delenv("PIXPATH_FFV1")
+    monkeypatch.delenv("PIXPATH_FFV1")  # the default: FFV1 on the GPU
+    assert pff._gpu_cli("cpvs", ["-y", "/c.avi"]).endswith("--gpu-ffv1 /c.avi")
+    monkeypatch.setenv("PIXPATH_FFV1", "ffmpeg")
     assert "--gpu-ffv1" not in pff._gpu_cli("cpvs", ["-y", "/c.avi"])
