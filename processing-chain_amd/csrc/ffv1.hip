@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <cstring>
 #include <memory>
+#include <type_traits>
 #include <vector>
 
 #include "common.hpp"
@@ -270,83 +271,116 @@ __device__ __host__ inline SliceGeo slice_geo(int g, int w, int h, int nh, int n
 }
 
 // ---- 1. modelling: tokens (context key << 16 | folded residual) -------------
-// One thread per (slice, plane row); 64 threads = the 64 lanes of one coder
-// wave.  key = plane set * 666 + |context|; the residual is negated with the
-// context (encode_line), folded to the bit depth, stored as int16.
+// One workgroup per (64-slice wave group, plane row); 64 threads = the coder
+// wave's 64 lanes.  The row and the row above of all 64 slices are staged in
+// LDS 64 columns at a time with coalesced loads (consecutive threads read
+// consecutive samples of one slice row), then each thread walks its own
+// slice's columns from LDS and stores one token per column -- the 64 threads'
+// stores of a column are one contiguous 256-B line.  key = plane set * 666 +
+// |context|; the residual is negated with the context (encode_line), folded
+// to the bit depth, stored as int16.
+constexpr int kMX = 64;          // columns per staged chunk
+constexpr int kMS = kMX + 3;     // staged samples per row: x0 - 1 .. x0 + 64 (+1); odd stride, no bank conflicts
 template <typename ST>
 __global__ __launch_bounds__(64) void ffv1_model_kernel(const Ffv1Args a) {
-    const int lane = threadIdx.x;
+    __shared__ int s_row[64][2][kMS];  // [lane][top, cur][column x0 - 1 + j]
+    const int t = threadIdx.x;
     const int wg = blockIdx.y;
-    const int g = wg * 64 + lane;
-    if (g >= a.nslices) return;
-    const SliceGeo q = slice_geo(g, a.w, a.h, a.nh, a.nv, a.hsub, a.vsub);
-    int r = blockIdx.x, p, off;
+    const int g = wg * 64 + t;
+    const bool live = g < a.nslices;
+    const SliceGeo q = slice_geo(live ? g : 0, a.w, a.h, a.nh, a.nv, a.hsub, a.vsub);
+    int r = blockIdx.x, p = 0, off = 0;
+    bool on = live;
     if (r < q.lh) {
-        p = 0; off = 0;
+        p = 0;
     } else if ((r -= q.lh) < q.ch) {
         p = 1; off = q.lw * q.lh;
     } else if ((r -= q.ch) < q.ch) {
         p = 2; off = q.lw * q.lh + q.cw * q.ch;
     } else {
-        return;
+        on = false;
     }
     const int y = r;
-    const int pw = p ? q.cw : q.lw;
+    const int pw = on ? (p ? q.cw : q.lw) : 0;
     const int px0 = p ? q.x0 >> a.hsub : q.x0, py0 = p ? q.y0 >> a.vsub : q.y0;
     const uint8_t *src = p == 0 ? a.src[0] : p == 1 ? a.src[1] : a.src[2];
     const int64_t ls = p == 0 ? a.ls[0] : p == 1 ? a.ls[1] : a.ls[2];
     const int64_t fs = p == 0 ? a.fs[0] : p == 1 ? a.fs[1] : a.fs[2];
-    const uint8_t *rowb = src + q.frame * fs + (int64_t)(py0 + y) * ls + (int64_t)px0 * sizeof(ST);
-    const ST *row = reinterpret_cast<const ST *>(rowb);
-    const ST *top = reinterpret_cast<const ST *>(rowb - ls);
+    // this lane's row start; broadcast per staged slice with readlane
+    const uint8_t *rowb = on ? src + q.frame * fs + (int64_t)(py0 + y) * ls + (int64_t)px0 * sizeof(ST) : src;
+    const uint64_t rowv = reinterpret_cast<uint64_t>(rowb);
+    const int hasT = on && y > 0;
     const int mask = (1 << a.bits) - 1, half = 1 << (a.bits - 1);
     const uint32_t key0 = p ? kFfv1Ctx : 0;
-    uint32_t *out = a.tok + ((int64_t)wg * a.tok_len + off + (int64_t)y * pw) * 64 + lane;
+    uint32_t *out = a.tok + ((int64_t)wg * a.tok_len + off + (int64_t)y * pw) * 64 + t;
     // FFmpeg's sample-buffer borders: 0 above the slice, L = T at column 0,
     // TL at column 0 = first sample two rows up, TR past the last column = T
-    int T = y > 0 ? top[0] : 0;
-    int TL = y > 1 ? reinterpret_cast<const ST *>(rowb - 2 * ls)[0] : 0;
-    int L = T;
-    int TR = pw > 1 ? (y > 0 ? top[1] : 0) : T;
-    for (int x = 0; x < pw; ++x) {
-        const int v = row[x];
-        int ctx = dquant((L - TL) & 0xFF) + 11 * dquant((TL - T) & 0xFF) + 121 * dquant((T - TR) & 0xFF);
-        int diff = v - median3(L, L + T - TL, T);
-        if (ctx < 0) {
-            ctx = -ctx;
-            diff = -diff;
+    const int TL0 = on && y > 1 ? reinterpret_cast<const ST *>(rowb - 2 * ls)[0] : 0;
+    int pw_max = pw;
+    for (int o = 32; o > 0; o >>= 1) pw_max = max(pw_max, __shfl_xor(pw_max, o));
+    int L = 0, TL = 0;
+    for (int x0 = 0; x0 < pw_max; x0 += kMX) {
+        __syncthreads();  // the previous chunk's LDS reads are done
+        // stage columns x0 - 1 .. x0 + 65 of the row and the row above of every slice
+        for (int j = 0; j < 64; ++j) {
+            const uint64_t rb = ((uint64_t)__builtin_amdgcn_readlane((int)(rowv >> 32), j) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rowv, j);
+            const int pwj = __builtin_amdgcn_readlane(pw, j), tj = __builtin_amdgcn_readlane(hasT, j);
+            const ST *rr = reinterpret_cast<const ST *>(rb);
+            for (int e = t; e < 2 * kMS; e += 64) {
+                const int rw = e >= kMS ? 1 : 0, col = e - rw * kMS, x = x0 - 1 + col;
+                int v = 0;
+                if (x >= 0 && x < pwj && (rw || tj)) v = rw ? rr[x] : reinterpret_cast<const ST *>(rb - ls)[x];
+                s_row[j][rw][col] = v;
+            }
         }
-        diff &= mask;
-        diff = diff >= half ? diff - (mask + 1) : diff;
-        out[(int64_t)x * 64] = ((key0 + (uint32_t)ctx) << 16) | ((uint32_t)diff & 0xFFFFu);
-        const int nTR = x + 2 < pw ? (y > 0 ? top[x + 2] : 0) : TR;
-        L = v;
-        TL = T;
-        T = TR;
-        TR = nTR;
+        __syncthreads();
+        const int xe = min(pw, x0 + kMX);
+        for (int x = x0; x < xe; ++x) {
+            const int c = x - x0 + 1;
+            const int T = s_row[t][0][c];
+            const int v = s_row[t][1][c];
+            if (x == 0) {
+                L = T;
+                TL = TL0;
+            }
+            const int TR = x + 1 < pw ? s_row[t][0][c + 1] : T;
+            int ctx = dquant((L - TL) & 0xFF) + 11 * dquant((TL - T) & 0xFF) + 121 * dquant((T - TR) & 0xFF);
+            int diff = v - median3(L, L + T - TL, T);
+            if (ctx < 0) {
+                ctx = -ctx;
+                diff = -diff;
+            }
+            diff &= mask;
+            diff = diff >= half ? diff - (mask + 1) : diff;
+            out[(int64_t)x * 64] = ((key0 + (uint32_t)ctx) << 16) | ((uint32_t)diff & 0xFFFFu);
+            L = v;
+            TL = T;
+        }
     }
 }
 
 // ---- 2. coding ---------------------------------------------------------------
 // The range coder of one lane.  renorm records, per output byte,
-// (low >> 8) | ((low & 0xFF) == 0) << 9 in a 16-bit slot (two per dword);
-// ffv1_resolve_kernel turns them into bytes exactly as renorm_encoder does.
+// (low >> 8) | ((low & 0xFF) == 0) << 9 as a 16-bit value in the lane's LDS
+// ring; ffv1_resolve_kernel turns them into bytes exactly as renorm_encoder
+// does.  Every coding step ends with one unconditional store of the ring's
+// oldest 16 records, so the number of vector-memory operations per step is a
+// constant and the wait for a block loaded two steps earlier can leave the
+// younger loads and stores in flight (vmcnt counts both, in order).
+constexpr int kRing = 64;    // records per lane ring (LDS)
+constexpr int kFlush = 16;   // records stored per step (2 x 16 B)
 struct Enc {
-    uint32_t low, range, acc, half;
-    uint32_t *out;
-    int n, cap;
+    uint32_t low, range;
+    uint16_t *ring;          // this lane's kRing records
+    uint32_t wp;             // records pushed
 };
 
 __device__ __forceinline__ void enc_renorm(Enc &c) {
     if (c.range < 0x100u) {
         const uint32_t raw = (c.low >> 8) | ((c.low & 0xFFu) == 0u ? 0x200u : 0u);
-        c.acc |= raw << c.half;
-        if (c.half) {
-            if (c.n < c.cap) c.out[c.n] = c.acc;
-            ++c.n;
-            c.acc = 0;
-        }
-        c.half ^= 16u;
+        c.ring[c.wp & (kRing - 1)] = (uint16_t)raw;
+        ++c.wp;
         c.low = (c.low & 0xFFu) << 8;
         c.range <<= 8;
     }
@@ -431,6 +465,7 @@ __device__ __forceinline__ void blk_sel(uint32_t (&d)[8], bool c, const uint32_t
 
 __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
     __shared__ uint8_t s_tab[512];  // zero[256], one[256]
+    __shared__ __align__(16) uint16_t s_ring[64 * kRing];
     for (int i = threadIdx.x; i < 512; i += 64) s_tab[i] = a.tables[i];
     __syncthreads();
     const int lane = threadIdx.x;
@@ -441,9 +476,23 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
     uint8_t *const st0 = a.states + (int64_t)g * kStateBytes;
     const uint32_t *tp = a.tok + (int64_t)blockIdx.x * a.tok_len * 64 + lane;
     Enc c;
-    c.low = 0; c.range = 0xFF00; c.acc = 0; c.half = 0;
-    c.out = a.raw + (int64_t)g * a.raw_cap;
-    c.n = 0; c.cap = (int)a.raw_cap;
+    c.low = 0; c.range = 0xFF00; c.wp = 0;
+    c.ring = s_ring + lane * kRing;
+    // records leave the ring kFlush at a time into the lane's record buffer;
+    // `fp` records are final there, the rest of the 16 is rewritten next step
+    uint8_t *const out = reinterpret_cast<uint8_t *>(a.raw + (int64_t)g * a.raw_cap);
+    const uint32_t cap = (uint32_t)(a.raw_cap * 2) & ~(uint32_t)(kFlush - 1);  // records the buffer holds
+    uint32_t fp = 0;
+    bool over = false;
+    auto flush = [&]() {
+        const uint4 *r = reinterpret_cast<const uint4 *>(c.ring + (fp & (kRing - 1)));
+        const uint4 x = r[0], y = r[1];
+        uint4 *d = reinterpret_cast<uint4 *>(out + 2 * (int64_t)(fp < cap ? fp : cap - kFlush));
+        d[0] = x;
+        d[1] = y;
+        over |= c.wp - fp > (uint32_t)(kRing - kFlush) || fp >= cap;
+        if (c.wp - fp >= (uint32_t)kFlush) fp += kFlush;
+    };
     // keyframe bit (first slice of a frame), then the slice header with its own 32 states:
     // slice x, y, width - 1, height - 1 (slice units), table set of Y and of Cb/Cr,
     // picture_structure 3 (progressive), SAR 1:1 (setsar=1/1)
@@ -456,31 +505,40 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
 #pragma unroll
         for (int i = 0; i < 9; ++i) enc_symbol<false>(c, hb, hv[i], s_tab);
     }
-    // token stream with block forwarding (see the file comment)
-    uint32_t t0 = len > 0 ? tp[0] : 0u, t1 = len > 1 ? tp[64] : 0u, t2 = len > 2 ? tp[128] : 0u,
-             t3 = len > 3 ? tp[192] : 0u;
+    // token stream with block forwarding (see the file comment); every step
+    // issues the same vector-memory operations: one token load, one block
+    // load, one block store, one ring flush
+    // (an unconditional load: past the end it rereads the last token, a valid key)
+    auto tok = [&](int i) { return tp[(int64_t)min(i, len - 1) * 64]; };
+    // tokens and prefetched blocks live in fixed registers (a ring indexed by
+    // the step's phase, 4x unrolled): a register copy of an in-flight load
+    // would make the compiler wait for it at the copy
+    uint32_t tk[4] = {tok(0), tok(1), tok(2), tok(3)};
     int km2 = -1, km1 = -1;
-    uint32_t cur[8], prev[8], pre0[8], pre1[8];
+    uint32_t cur[8], prev[8], pre[2][8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) cur[i] = prev[i] = 0u;
-    if (len > 0) blk_load(pre0, st0 + (t0 >> 16) * kCtxSize);
-    if (len > 1 && (t1 >> 16) != (t0 >> 16)) blk_load(pre1, st0 + (t1 >> 16) * kCtxSize);
-    auto step = [&](int i, uint32_t (&pre)[8]) {
+    blk_load(pre[0], st0 + (tk[0] >> 16) * kCtxSize);
+    blk_load(pre[1], st0 + (tk[1] >> 16) * kCtxSize);
+    auto step = [&](int i, auto ph_c) {
+        constexpr int PH = decltype(ph_c)::value;
+        const uint32_t t0 = tk[PH], t1 = tk[(PH + 1) & 3], t2 = tk[(PH + 2) & 3];
         const int k0 = (int)(t0 >> 16);
         const int v = (int)(int16_t)(t0 & 0xFFFFu);
         uint32_t b[8];
         // block of this sample: the previous sample's, the one before, or the prefetched
         {
             uint32_t tmp[8];
-            blk_sel(tmp, k0 == km2, prev, pre);
+            blk_sel(tmp, k0 == km2, prev, pre[PH & 1]);
             blk_sel(b, k0 == km1, cur, tmp);
         }
-        // prefetch the block of sample i + 2 unless one of samples i, i + 1 forwards it
-        const int k1 = (int)(t1 >> 16), k2 = (int)(t2 >> 16);
-        if (i + 2 < len && k2 != k0 && k2 != k1) blk_load(pre, st0 + k2 * kCtxSize);
-        const uint32_t tn = i + 4 < len ? tp[(int64_t)(i + 4) * 64] : 0u;
+        // the block of sample i + 2 (used unless sample i or i + 1 forwards it)
+        blk_load(pre[PH & 1], st0 + (t2 >> 16) * kCtxSize);
+        tk[PH] = tok(i + 4);
+        (void)t1;
         enc_symbol<true>(c, b, v, s_tab);
-        if (i + 1 < len && k1 != k0) blk_store(st0 + k0 * kCtxSize, b);
+        blk_store(st0 + k0 * kCtxSize, b);
+        flush();
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             prev[j] = cur[j];
@@ -488,14 +546,17 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
         }
         km2 = km1;
         km1 = k0;
-        t0 = t1; t1 = t2; t2 = t3; t3 = tn;
     };
     int i = 0;
-    for (; i + 1 < len; i += 2) {
-        step(i, pre0);
-        step(i + 1, pre1);
+    for (; i + 3 < len; i += 4) {
+        step(i, std::integral_constant<int, 0>{});
+        step(i + 1, std::integral_constant<int, 1>{});
+        step(i + 2, std::integral_constant<int, 2>{});
+        step(i + 3, std::integral_constant<int, 3>{});
     }
-    if (i < len) step(i, pre0);
+    if (i < len) step(i, std::integral_constant<int, 0>{});
+    if (i + 1 < len) step(i + 1, std::integral_constant<int, 1>{});
+    if (i + 2 < len) step(i + 2, std::integral_constant<int, 2>{});
     // closing 0 bit at state 129 (ffv1enc.c encode_frame), ff_rac_terminate's two flushes
     (void)enc_rac(c, 129, 0, s_tab);
     c.range = 0xFF;
@@ -503,12 +564,14 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
     enc_renorm(c);
     c.range = 0xFF;
     enc_renorm(c);
-    const int nraw = 2 * c.n + (c.half ? 1 : 0);
-    if (c.half) {
-        if (c.n < c.cap) c.out[c.n] = c.acc;
-        ++c.n;
+    while (fp < c.wp) {
+        flush();
+        if (c.wp - fp < (uint32_t)kFlush) {  // the partial tail is stored; done
+            flush();
+            break;
+        }
     }
-    a.nraw[g] = c.n > c.cap ? -1 : nraw;
+    a.nraw[g] = over || c.wp > cap ? -1 : (int32_t)c.wp;
 }
 
 // ---- 3. bytes: renorm_encoder's outstanding-byte machine ----------------------

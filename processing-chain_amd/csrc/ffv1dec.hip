@@ -30,7 +30,6 @@ namespace {
 
 constexpr int kCtx = 32;
 constexpr int kMaxCtx = 4096;              // context count the state blocks are sized for
-constexpr int kSlot = 40;
 
 struct HostRD {
     int low = 0, range = 0xFF00;
@@ -93,54 +92,108 @@ struct Ffv1DecArgs {
     const int16_t *quant;        // [3][256] (scaled)
 };
 
-struct DevRD {
-    int low, range;
+// The slice's range decoder (rangecoder.h get_rac / refill) on register-held
+// state: a symbol's state bytes come from the current context's 32-byte block
+// in 8 VGPRs (all read before its first decision, updated bytes written after
+// the last, so the LDS state-table lookups never sit on the low/range chain).
+struct Dec {
+    uint32_t low, range;
     const uint8_t *p, *end;
-    const uint8_t *zero, *one;
-    __device__ __forceinline__ void refill() {
-        if (range < 0x100) {
-            range <<= 8;
-            low <<= 8;
-            if (p < end) low += *p++;
-        }
-    }
-    __device__ __forceinline__ int rac(uint8_t *st) {
-        const int sv = *st;
-        const int r1 = (range * sv) >> 8;
-        range -= r1;
-        if (low < range) {
-            *st = zero[sv];
-            refill();
-            return 0;
-        }
-        low -= range;
-        *st = one[sv];
-        range = r1;
-        refill();
-        return 1;
-    }
-    __device__ __forceinline__ int symbol(uint8_t *st, bool is_signed) {
-        if (rac(st)) return 0;
-        int e = 0;
-        while (rac(st + 1 + min(e, 9))) {
-            if (++e > 31) return 0;
-        }
-        int a = 1;
-        for (int i = e - 1; i >= 0; i--) a += a + rac(st + 22 + min(i, 9));
-        return (is_signed && rac(st + 11 + min(e, 10))) ? -a : a;
-    }
 };
+
+__device__ __forceinline__ void dec_refill(Dec &d) {
+    if (d.range < 0x100u) {
+        d.range <<= 8;
+        d.low <<= 8;
+        if (d.p < d.end) d.low += *d.p++;
+    }
+}
+
+// one decision with state value s; ns receives the next state value
+__device__ __forceinline__ uint32_t dec_rac(Dec &d, uint32_t s, const uint8_t *tab, uint32_t &ns) {
+    const uint32_t r1 = __umul24(d.range, s) >> 8;
+    const uint32_t r0 = d.range - r1;
+    const uint32_t bit = d.low >= r0 ? 1u : 0u;
+    d.low -= bit ? r0 : 0u;
+    d.range = bit ? r1 : r0;
+    ns = tab[s | (bit << 8)];
+    dec_refill(d);
+    return bit;
+}
+
+__device__ __forceinline__ uint32_t dsget(const uint32_t (&b)[8], int k) { return (b[k >> 2] >> ((k & 3) * 8)) & 0xFFu; }
+__device__ __forceinline__ void dsput(uint32_t (&b)[8], int k, uint32_t v) {
+    b[k >> 2] = (b[k >> 2] & ~(0xFFu << ((k & 3) * 8))) | (v << ((k & 3) * 8));
+}
+__device__ __forceinline__ uint32_t dsget_dyn(const uint32_t (&b)[8], int k) {  // k in 8..23
+    const int w = k >> 2;
+    const uint32_t x = w == 2 ? b[2] : w == 3 ? b[3] : w == 4 ? b[4] : b[5];
+    return (x >> ((k & 3) * 8)) & 0xFFu;
+}
+__device__ __forceinline__ void dsput_dyn(uint32_t (&b)[8], int k, uint32_t v) {
+    const int w = k >> 2;
+    const uint32_t sh = (k & 3) * 8, m = ~(0xFFu << sh), nv = v << sh;
+    b[2] = w == 2 ? (b[2] & m) | nv : b[2];
+    b[3] = w == 3 ? (b[3] & m) | nv : b[3];
+    b[4] = w == 4 ? (b[4] & m) | nv : b[4];
+    b[5] = w == 5 ? (b[5] & m) | nv : b[5];
+}
+
+// get_symbol (ffv1dec.c) for samples of <= 10 bits: exponent e <= 9, so
+// every state index is used at most once per symbol; e >= 10 (not a <= 10-bit
+// stream) sets `bad`.
+template <bool SIGNED>
+__device__ __forceinline__ int dec_symbol(Dec &d, uint32_t (&b)[8], const uint8_t *tab, bool &bad) {
+    uint32_t n0;
+    const uint32_t z = dec_rac(d, dsget(b, 0), tab, n0);
+    uint32_t nu[10], nm[9], nsg = 0;
+    int e = 0, a = 1;
+    uint32_t neg = 0;
+    if (!z) {
+        bool go = true;
+#pragma unroll
+        for (int i = 0; i < 10; ++i)
+            if (go) {
+                if (dec_rac(d, dsget(b, 1 + i), tab, nu[i])) e = i + 1;
+                else go = false;
+            }
+        if (go) bad = true;
+#pragma unroll
+        for (int i = 8; i >= 0; --i)
+            if (i < e) a = 2 * a + (int)dec_rac(d, dsget(b, 22 + i), tab, nm[i]);
+        if constexpr (SIGNED) neg = dec_rac(d, dsget_dyn(b, 11 + min(e, 9)), tab, nsg);
+    }
+    dsput(b, 0, n0);
+    if (!z) {
+#pragma unroll
+        for (int i = 0; i < 10; ++i)
+            if (i <= e) dsput(b, 1 + i, nu[i]);
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+            if (i < e) dsput(b, 22 + i, nm[i]);
+        if constexpr (SIGNED) dsput_dyn(b, 11 + min(e, 9), nsg);
+    }
+    return z ? 0 : (neg ? -a : a);
+}
+
+__device__ __forceinline__ void dblk_load(uint32_t (&b)[8], const uint8_t *p) {
+    const uint4 x = reinterpret_cast<const uint4 *>(p)[0], y = reinterpret_cast<const uint4 *>(p)[1];
+    b[0] = x.x; b[1] = x.y; b[2] = x.z; b[3] = x.w; b[4] = y.x; b[5] = y.y; b[6] = y.z; b[7] = y.w;
+}
+__device__ __forceinline__ void dblk_store(uint8_t *p, const uint32_t (&b)[8]) {
+    reinterpret_cast<uint4 *>(p)[0] = make_uint4(b[0], b[1], b[2], b[3]);
+    reinterpret_cast<uint4 *>(p)[1] = make_uint4(b[4], b[5], b[6], b[7]);
+}
 
 __device__ __forceinline__ int dmedian3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 
 __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
-    __shared__ uint8_t s_zero[256], s_one[256];
+    __shared__ uint8_t s_tab[512];  // zero[256], one[256]
     __shared__ uint32_t s_crc[256];
     __shared__ int16_t s_q[3][256];
-    __shared__ __align__(16) uint8_t s_ctx[64 * kSlot];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-        s_zero[i] = a.tables[i];
-        s_one[i] = a.tables[256 + i];
+        s_tab[i] = a.tables[i];
+        s_tab[256 + i] = a.tables[256 + i];
         s_crc[i] = reinterpret_cast<const uint32_t *>(a.tables + 512)[i];
         s_q[0][i] = a.quant[i];
         s_q[1][i] = a.quant[256 + i];
@@ -162,48 +215,37 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
         }
     }
     uint8_t *const st0 = a.states + (int64_t)g * a.state_bytes;
-    uint8_t *const hs = st0 + 2 * (int64_t)a.ctx_count * kCtx;
-    DevRD d;
-    d.zero = s_zero; d.one = s_one;
+    Dec d;
     d.p = sb; d.end = sb + n; d.range = 0xFF00;
-    d.low = n >= 2 ? (sb[0] << 8) | sb[1] : 0;
+    d.low = n >= 2 ? ((uint32_t)sb[0] << 8) | sb[1] : 0;
     d.p += 2;
-    if (d.low >= 0xFF00) { d.low = 0xFF00; d.end = d.p; }
-    if (s == 0 && !d.rac(hs + 32)) {  // keyframe bit
+    if (d.low >= 0xFF00u) { d.low = 0xFF00u; d.end = d.p; }
+    uint32_t dummy;
+    if (s == 0 && !dec_rac(d, 128, s_tab, dummy)) {  // keyframe bit
         a.status[g] = 2;
         return;
     }
-    const int sx = d.symbol(hs, false), sy = d.symbol(hs, false);
-    const int sw = d.symbol(hs, false) + 1, sh = d.symbol(hs, false) + 1;
-    const int q0 = d.symbol(hs, false), q1 = d.symbol(hs, false), ps = d.symbol(hs, false);
-    d.symbol(hs, false);
-    d.symbol(hs, false);  // sample aspect ratio
-    if (sx < 0 || sy < 0 || sx > a.nh - sw || sy > a.nv - sh || q0 || q1 || ps != 3) {
+    bool bad = false;
+    int hv[9];
+    {
+        uint32_t hb[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) hb[i] = 0x80808080u;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) hv[i] = dec_symbol<false>(d, hb, s_tab, bad);
+    }
+    const int sx = hv[0], sy = hv[1], sw = hv[2] + 1, sh = hv[3] + 1;
+    if (bad || sx < 0 || sy < 0 || sx > a.nh - sw || sy > a.nv - sh || hv[4] || hv[5] || hv[6] != 3) {
         a.status[g] = 2;
         return;
     }
     const int x0 = (int)((int64_t)sx * a.w / a.nh), x1 = (int)((int64_t)(sx + sw) * a.w / a.nh);
     const int y0 = (int)((int64_t)sy * a.h / a.nv), y1 = (int)((int64_t)(sy + sh) * a.h / a.nv);
     const int mask = (1 << a.bits) - 1;
-    uint8_t *const slot = s_ctx + threadIdx.x * kSlot;
     int cur_key = -1;
-    auto use_ctx = [&](int key) {
-        if (key == cur_key) return;
-        if (cur_key >= 0) {
-            uint2 *gp = reinterpret_cast<uint2 *>(st0 + cur_key * kCtx);
-            const uint2 *l = reinterpret_cast<const uint2 *>(slot);
+    uint32_t blk[8];
 #pragma unroll
-            for (int i = 0; i < 4; i++) gp[i] = l[i];
-        }
-        const uint2 *gp = reinterpret_cast<const uint2 *>(st0 + key * kCtx);
-        uint2 *l = reinterpret_cast<uint2 *>(slot);
-        uint2 v[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) v[i] = gp[i];
-#pragma unroll
-        for (int i = 0; i < 4; i++) l[i] = v[i];
-        cur_key = key;
-    };
+    for (int i = 0; i < 8; ++i) blk[i] = 0u;
     for (int p = 0; p < 3; p++) {
         const int pw = p ? ((x1 - x0) + (1 << a.hsub) - 1) >> a.hsub : x1 - x0;
         const int ph = p ? ((y1 - y0) + (1 << a.vsub) - 1) >> a.vsub : y1 - y0;
@@ -222,13 +264,20 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
             int T = y > 0 ? ld(top, 0) : 0;
             int TL = y > 1 ? ld(top2, 0) : 0;
             int L = T;
+            // the row above two columns ahead, loaded a sample early
+            int TR = pw > 1 ? (y > 0 ? ld(top, 1) : 0) : T;
             for (int x = 0; x < pw; x++) {
-                const int TR = x + 1 < pw ? (y > 0 ? ld(top, x + 1) : 0) : T;
+                const int nTR = x + 2 < pw ? (y > 0 ? ld(top, x + 2) : 0) : TR;
                 int ctx = s_q[0][(L - TL) & 0xFF] + s_q[1][(TL - T) & 0xFF] + s_q[2][(T - TR) & 0xFF];
                 const bool neg = ctx < 0;
                 if (neg) ctx = -ctx;
-                use_ctx(key0 + ctx);
-                int diff = d.symbol(slot, true);
+                const int key = key0 + ctx;
+                if (key != cur_key) {
+                    if (cur_key >= 0) dblk_store(st0 + cur_key * kCtx, blk);
+                    dblk_load(blk, st0 + key * kCtx);
+                    cur_key = key;
+                }
+                int diff = dec_symbol<true>(d, blk, s_tab, bad);
                 if (neg) diff = -diff;
                 const int v = (dmedian3(L, L + T - TL, T) + diff) & mask;
                 if (a.bytes == 2)
@@ -237,13 +286,13 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
                     row[x] = (uint8_t)v;
                 TL = T;
                 T = TR;
+                TR = nTR;
                 L = v;
             }
         }
     }
-    hs[33] = 129;
-    d.rac(hs + 33);
-    a.status[g] = ((d.end - d.p) - 2 - 5 * (a.ec != 0)) != 0 ? 3 : 0;
+    (void)dec_rac(d, 129, s_tab, dummy);  // the closing bit at state 129
+    a.status[g] = bad ? 2 : ((d.end - d.p) - 2 - 5 * (a.ec != 0)) != 0 ? 3 : 0;
 }
 
 }  // namespace pp

@@ -731,18 +731,18 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
     }
     // strip_kernel eligibility: the generic tiling fits 256-column strips,
     // <= 8 V tap pairs, one H window bucket for both planes, single-pass
-    // staging, LDS within the budget.  Strip width: 512 (8 waves) for plain
-    // plans when it fits (twice the budget: the same waves per CU), else 256;
-    // chain and packed plans keep 256.  PIXPATH_STRIP_TW=256|512 overrides
-    // (measurement only).
+    // staging, LDS within the budget.  Strip width 256; PIXPATH_STRIP_TW=512
+    // (plain plans only, measurement) runs 512-column strips with 8 waves and
+    // twice the LDS budget -- measured slower on every config (config 2
+    // 1.554 vs 1.501 ms, config 3 10-bit 5.17 vs 4.87 ms, 8-bit 3.57 vs
+    // 3.25 ms per 600-frame launch; profiles/r3/strip_tw_ab.txt).
     {
         const char *force = std::getenv("PIXPATH_SCALE_KERNEL");
         const char *etw = std::getenv("PIXPATH_STRIP_TW");
         bool ok0 = !(force && std::strcmp(force, "generic") == 0);
         const int CH = si.depth > 8 ? 8 : 16;
         for (int c = 0; c < 2 && ok0; ++c) ok0 = hp[c].tw == kTileW && hp[c].vtp <= 8;
-        int tw_first = (one_seg_chroma || di.packed) ? 256 : 512;
-        if (etw) tw_first = atoi(etw) == 512 ? 512 : 256;
+        const int tw_first = (etw && atoi(etw) == 512 && !one_seg_chroma && !di.packed) ? 512 : 256;
         for (int ftw = tw_first; ok0 && ftw >= 256; ftw /= 2) {
             bool ok = true;
             int need = 1;
@@ -974,8 +974,9 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
         *out = P.release();
         return PP_OK;
     }
-    if (!ctx) {  // host-only plan: introspection (pp_scale_plan_path) only
+    if (!ctx) {  // host-only plan: introspection (pp_scale_plan_path / _stats) only
         P->chain_fused = true;
+        P->chain_lds = lds;
         *out = P.release();
         return PP_OK;
     }
@@ -1022,7 +1023,9 @@ extern "C" int pp_scale_plan_stats(const pp_scale_plan *P, int64_t *out, int n) 
     if (P->kind == pp_scale_plan::COPY || P->kind == pp_scale_plan::INTERLEAVE) return 0;
     const bool strip = P->fast_hw > 0;
     const pp::PlaneJob &L = strip ? P->fjob[0] : P->job[0];
-    const int64_t v[] = {(int64_t)(strip ? P->fast_lds : P->lds_bytes), strip ? P->fast_tw : pp::kThreads,
+    const bool chain = P->kind == pp_scale_plan::CHAIN && P->chain_fused;
+    const int64_t v[] = {(int64_t)(chain ? P->chain_lds : strip ? P->fast_lds : P->lds_bytes),
+                         strip ? P->fast_tw : pp::kThreads,
                          strip ? P->fast_tiles : P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y, L.cho,
                          L.seg_h, L.vtp,
                          P->job[1].vtp, L.S, L.ring, L.maxnew};

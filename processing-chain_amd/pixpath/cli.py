@@ -10,6 +10,7 @@ the ffmpeg strings they replace).
          (create_cpvs PC branch lib/ffmpeg.py:1177-1201)
   stall  AVPVS -> stall frames (frozen/black + spinner) or frame freezing
          (bufferer call p03_generateAvPvs.py:236-243, spec PP-STALL-1)
+  concat long-test segment AVIs -> one AVI, packets copied (create_avpvs_long_concat :1058, GPU-FFV1 AVIs)
   siti   P.910 SI/TI of a SRC (util/SRC_analysis.py hook)
 
 Inputs/outputs ending in .y4m or .raw/.yuv are read/written directly;
@@ -540,6 +541,45 @@ def cmd_stall(args):
     return 0
 
 
+def cmd_concat(args):
+    """create_avpvs_long_concat (lib/ffmpeg.py:1058-1105: `ffmpeg -f concat
+    -safe 0 -i <filelist> -c:v copy -t <total>`) for GPU-FFV1 AVIs: the
+    segment canvases' packets copied in filelist order (all-intra FFV1, one
+    configuration record), cut after round(total * rate) frames.  No pixels
+    are decoded."""
+    from . import avi
+    out = args.output
+    if _skip(out, args.y):
+        return 0
+    files = []
+    with open(args.filelist) as fh:
+        for line in fh:
+            line = line.strip()
+            if line.startswith("file "):
+                files.append(line[5:].strip().strip("'"))
+    if not files:
+        raise SystemExit("pixpath concat: %s lists no files" % args.filelist)
+    scans = [avi.scan(f) for f in files]
+    i0 = scans[0][0]
+    for f, (info, _) in zip(files, scans):
+        if info.get("fourcc") != b"FFV1" or info.get("extradata") != i0.get("extradata") or \
+                (info["w"], info["h"], info["rate"]) != (i0["w"], i0["h"], i0["rate"]):
+            raise SystemExit("pixpath concat: %s is not a GPU-FFV1 AVI matching %s" % (f, files[0]))
+    cap = int(round(Fraction(str(args.duration)) * i0["rate"])) if args.duration else None
+    wr = avi.AviWriter(out, i0["w"], i0["h"], i0["rate"], extradata=i0["extradata"])
+    n = 0
+    for f, (_, index) in zip(files, scans):
+        with open(f, "rb") as fh:
+            for off, size in index:
+                if cap is not None and n >= cap:
+                    break
+                fh.seek(off)
+                wr.write_packet(fh.read(size))
+                n += 1
+    wr.close()
+    return 0
+
+
 def _black(fmt, w, h):
     from . import formats, io as pio
     planes = [np.full((1, r, c), (16 if p == 0 else 128) << (fmt.depth - 8),
@@ -630,6 +670,15 @@ def main(argv=None):
     p.add_argument("--black-frame", action="store_true")
     p.add_argument("--gpu-ffv1", action="store_true", help="FFV1 AVI in and out, coded on the GPU")
     p.set_defaults(fn=cmd_stall)
+
+    p = sub.add_parser("concat")
+    g = p.add_mutually_exclusive_group()
+    g.add_argument("-y", action="store_true", help="overwrite output")
+    g.add_argument("-n", action="store_true", help="never overwrite (default)")
+    p.add_argument("--filelist", required=True)
+    p.add_argument("--duration", default=None)
+    p.add_argument("output")
+    p.set_defaults(fn=cmd_concat)
 
     p = sub.add_parser("siti")
     p.add_argument("--input", required=True)

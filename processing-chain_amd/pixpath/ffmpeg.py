@@ -312,8 +312,10 @@ def create_avpvs_segment(seg, pvs, overwrite=False, scale_avpvs_tosource=False):
 
 def create_avpvs_long_concat(pvs, overwrite=False, scale_avpvs_tosource=False):
     """Stream-copy concat of the decoded segments (lib/ffmpeg.py:1058-1105); writes the
-    concat file list as a side effect, like the reference.  No pixel work: both
-    backends return the same ffmpeg string."""
+    concat file list as a side effect, like the reference.  No pixel work: the
+    ffmpeg backend (and the gpu backend with PIXPATH_FFV1=ffmpeg) return the
+    reference's string; with the segment canvases written as GPU-FFV1 AVIs the
+    gpu backend copies their packets (`pixpath.cli concat`, same -t cut)."""
     output_file = pvs.get_tmp_wo_audio_path()
     overwrite_spec, skip = _skip_existing(output_file, overwrite)
     if skip:
@@ -323,6 +325,9 @@ def create_avpvs_long_concat(pvs, overwrite=False, scale_avpvs_tosource=False):
     with open(tmp_filelist, "w+") as fh:
         for s in pvs.segments:
             fh.write("file " + s.get_tmp_path() + "\n")
+    if _backend == "gpu" and ffv1_on_gpu():
+        return _collapse(_gpu_cli("concat", [overwrite_spec, "--filelist", tmp_filelist, "--duration", total,
+                                             output_file]))
     cmd = """
     ffmpeg -nostdin
     {overwrite_spec}

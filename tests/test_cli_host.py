@@ -1,5 +1,7 @@
 """Host-side pieces of the GPU pipeline (CPU): Y4M/raw I/O, stall schedule
 (PP-STALL-1), fps duplication counts == the vf_fps map."""
+import os
+
 import numpy as np
 import pytest
 
@@ -108,3 +110,71 @@ def test_gpu_ffv1_opt_in_flags(monkeypatch):
     assert pff._gpu_cli("cpvs", ["-y", "/c.avi"]).endswith("--gpu-ffv1 /c.avi")
     monkeypatch.setenv("PIXPATH_FFV1", "ffmpeg")
     assert "--gpu-ffv1" not in pff._gpu_cli("cpvs", ["-y", "/c.avi"])
+
+
+def test_cli_concat_copies_packets_and_cuts(tmp_path):
+    """`cli concat` (gpu backend's create_avpvs_long_concat for GPU-FFV1
+    segment AVIs): packets of the listed AVIs in order, cut at
+    round(duration * rate) frames like `-t`, same configuration record."""
+    from fractions import Fraction
+    from pixpath import avi, cli
+    rng = np.random.default_rng(5)
+    extra = b"cfg-record"
+    files, allp = [], []
+    for k in range(3):
+        p = str(tmp_path / ("tmp_seg%d.avi" % k))
+        w = avi.AviWriter(p, 64, 36, 60, extradata=extra)
+        for _ in range(120):
+            pk = rng.integers(0, 256, int(rng.integers(5, 300)), dtype=np.uint8).tobytes()
+            w.write_packet(pk)
+            allp.append(pk)
+        w.close()
+        files.append(p)
+    lst = str(tmp_path / "list.txt")
+    with open(lst, "w") as f:
+        f.writelines("file %s\n" % p for p in files)
+    out = str(tmp_path / "concat.avi")
+    assert cli.main(["concat", "-y", "--filelist", lst, "--duration", "5", out]) == 0
+    info, got = avi.read_packets(out)
+    assert got == allp[:300] and info["extradata"] == extra and info["rate"] == Fraction(60)
+    assert cli.main(["concat", "-y", "--filelist", lst, out]) == 0
+    assert avi.read_packets(out)[1] == allp
+    bad = str(tmp_path / "bad.avi")
+    w = avi.AviWriter(bad, 64, 36, 60, extradata=b"other")
+    w.write_packet(b"x")
+    w.close()
+    with open(lst, "a") as f:
+        f.write("file %s\n" % bad)
+    with pytest.raises(SystemExit):
+        cli.main(["concat", "-y", "--filelist", lst, out])
+
+
+def test_gpu_backend_long_concat_string(tmp_path, monkeypatch):
+    """gpu backend + GPU FFV1: create_avpvs_long_concat writes the reference's
+    filelist and returns `pixpath.cli concat` with the same -t total."""
+    import shlex
+    import ref_stubs
+    from test_host_reference_parity import Methods
+    from pixpath import ffmpeg as pff
+    sc = {"type": "long", "src": [3840, 2160], "segments": [[1280, 720, 2], [1280, 720, 3]],
+          "pps": [["pc", 1920, 1080]], "target_pix_fmt": "yuv422p10le",
+          "events": [["quality_level", 2], ["quality_level", 3]], "pvs_id": "P2LXM00_SRC001_HRC001"}
+    tc, pvs, _ = ref_stubs.build(sc, str(tmp_path), Methods)
+    os.makedirs(os.path.join(str(tmp_path), "avpvs"), exist_ok=True)
+    tc.root = str(tmp_path)
+    pff.set_backend("gpu")
+    try:
+        got = pff.create_avpvs_long_concat(pvs, overwrite=True)
+    finally:
+        pff.set_backend("ffmpeg")
+    a = shlex.split(got)
+    i = a.index("concat")
+    assert a[i + 1] == "-y" and a[a.index("--filelist") + 1] == pvs.get_avpvs_file_list()
+    assert a[a.index("--duration") + 1] == "5" and a[-1] == pvs.get_tmp_wo_audio_path()
+    assert open(pvs.get_avpvs_file_list()).read().count("file ") == 2
+    monkeypatch.setenv("PIXPATH_FFV1", "ffmpeg")
+    pff.set_backend("gpu")
+    try:
+        assert pff.create_avpvs_long_concat(pvs, overwrite=True).startswith("ffmpeg -nostdin -y -f concat")
+    finally:
+        pff.set_backend("ffmpeg")

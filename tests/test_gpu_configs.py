@@ -191,3 +191,50 @@ def test_config4_long_test_chain(gpu, tmp_path):
                      cpvs]) == 0
     os.remove(final)
     _v210_check(cpvs, ref, len(seq))
+
+
+def test_config4_long_test_through_gpu_ffv1(gpu, tmp_path):
+    """Config 4 with the gpu backend's default AVPVS codec (FFV1 on the GPU,
+    pixpath AVIs): create_avpvs_segment -> GPU-FFV1 canvases, the concat is a
+    packet copy (`cli concat`), the bufferer step works at the packet level
+    (pass-through frames copied, only the stall frames composed and encoded),
+    and the PC CPVS decodes on the GPU.  Every v210 frame equals the oracle's
+    two-stage chain + PP-STALL-1 + v210; the pass-through packets of the
+    stalled AVPVS are the concat's packets byte for byte: after the segment
+    encode no frame is decoded and re-encoded except the stalls' sources."""
+    from pixpath import avi, cli, spinner
+    rate, seg_s, n_seg = 60, 2, 3
+    per = seg_s * rate
+    rng = np.random.default_rng(404)
+    segs = [[synth.noise_frame(rng, po.YUV422P10LE, 960, 540) for _ in range(per)] for _ in range(n_seg)]
+    lst = str(tmp_path / "PVS_tmp_filelist.txt")
+    with open(lst, "w") as fl:
+        for i, frames in enumerate(segs):
+            s = str(tmp_path / ("seg%d.y4m" % i))
+            _write_y4m(s, "yuv422p10le", frames, 960, 540)
+            t = str(tmp_path / ("tmp_seg%d.avi" % i))
+            assert cli.main(["avpvs", "-y", "--input", s, "--size", "1920x1080", "--pix-fmt", "yuv422p10le",
+                             "--fps", "60", "--duration", str(seg_s), "--overlay-yuv420", "--aopts=-an",
+                             "--gpu-ffv1", t]) == 0
+            os.remove(s)
+            fl.write("file %s\n" % t)
+    concat = str(tmp_path / "PVS_concat_wo_buffer.avi")
+    assert cli.main(["concat", "-y", "--filelist", lst, "--duration", str(n_seg * seg_s), concat]) == 0
+    final = str(tmp_path / "PVS.avi")
+    assert cli.main(["stall", "-y", "--input", concat, "--buffer", "[[2,1.5],[4,1.0]]", "--spinner", GOLDEN_SPINNER,
+                     "--black-frame", "--aopts=-an", "--gpu-ffv1", final]) == 0
+    anim, delays = spinner.load_apng(GOLDEN_SPINNER)
+    seq = cli.stall_schedule([[2, 1.5], [4, 1.0]], rate, n_seg * per, False, delays)
+    _, pc = avi.read_packets(concat)
+    _, pf = avi.read_packets(final)
+    assert len(pc) == n_seg * per and len(pf) == len(seq)
+    assert all(pf[k] == pc[s] for k, (s, sp) in enumerate(seq) if sp < 0)
+    cpvs = str(tmp_path / "PVS_PC.raw")
+    assert cli.main(["cpvs", "-y", "--input", final, "--fps", "60", "--vcodec", "v210", "--pix-fmt", "yuv422p10le",
+                     "--gpu-ffv1", cpvs]) == 0
+
+    def concat_ref(k):
+        f = segs[k // per][k % per]
+        mid = po.scale(po.YUV422P10LE, f, po.YUV420P, 1920, 1080, po.SWS_BICUBIC)
+        return po.scale(po.YUV420P, mid, po.YUV422P10LE, 1920, 1080, po.SWS_BICUBIC)
+    _v210_check(cpvs, _stall_ref(concat_ref, anim, seq, po.YUV422P10LE), len(seq))

@@ -25,7 +25,8 @@ def _batch(gpu, name, frames):
 
 
 @pytest.mark.parametrize("name,fid,bits,hs,vs", CASES, ids=[c[0] for c in CASES])
-@pytest.mark.parametrize("w,h,grid", [(640, 360, (4, 4)), (330, 190, (3, 2)), (1920, 1080, (4, 4))])
+@pytest.mark.parametrize("w,h,grid", [(640, 360, (4, 4)), (330, 190, (3, 2)), (1920, 1080, (4, 4)),
+                                      (640, 360, (8, 8)), (1280, 720, (16, 16)), (200, 90, (7, 5))])
 def test_gpu_packets_match_oracle(gpu, name, fid, bits, hs, vs, w, h, grid):
     from pixpath import ffv1
     rng = np.random.default_rng(w + h)
@@ -233,6 +234,11 @@ def test_packet_level_stall_matches_oracle(gpu, tmp_path, skipping, buf):
     seq = stall.stall_schedule(ast.literal_eval(buf), 60, n, skipping, delays, True)
     assert len(pout) == len(seq)
     scaled = [po.scale(fid, f, fid, 640, 360, po.SWS_BICUBIC) for f in frames]
+    for k in range(n):  # the AVPVS itself: every packet decodes to the scaled frame
+        rc, dec = ref.decode_frame(iw["extradata"], pin[k], 640, 360, 8, 1, 1)
+        assert rc == 0
+        for p in range(3):
+            np.testing.assert_array_equal(dec[p], scaled[k][p], err_msg="AVPVS frame %d plane %d" % (k, p))
     yuva = {}
     for k, (s, sp) in enumerate(seq):
         if sp < 0 and s >= 0:
