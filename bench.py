@@ -362,6 +362,7 @@ def e2e_avpvs(wl, n_frames, dev):
             t0 = time.perf_counter()
             wr = Ffv1AviWriter(path, dfmt, dw, dh, 60, slices=(8, 8), batch=n_frames, device=dev.index)
             n = pl.run(MemReader(), wr)
+            t_pipe = time.perf_counter() - t0
             wr.close()
             dt = time.perf_counter() - t0
         size = os.path.getsize(path)
@@ -370,6 +371,8 @@ def e2e_avpvs(wl, n_frames, dev):
             os.remove(path)
         os.rmdir(d)
     return {"frames_per_s": round(n / dt, 1), "frames": n, "seconds": round(dt, 3), "avi_bytes": size,
+            "breakdown_s": {"host_to_scaled_in_hbm": round(t_pipe, 3), "ffv1_encode_and_d2h": round(wr.stats["encode_s"], 3),
+                            "avi_write": round(wr.stats["write_s"], 3)},
             "compression": round(n * frame_bytes(dfmt, dw, dh) / size, 3),
             "note": "host frames -> pinned batches of 60 -> H2D -> strip_kernel (720p->1080p yuv422p10le lanczos) "
                     "-> FFV1 v3 encode on the device output (8x8 slices, one 600-frame batch) -> packets D2H -> "

@@ -163,6 +163,7 @@ class Ffv1AviWriter:
         self.put_stream = torch.cuda.Stream(self.device)  # host-frame uploads
         self.avi = avi.AviWriter(path, w, h, rate, extradata=self.enc.extradata)
         self.frames = 0
+        self.stats = {"encode_s": 0.0, "write_s": 0.0, "bytes": 0}  # worker-thread time per part
         self.last_stream = self.put_stream
         self.q = queue.Queue()
         self.err = []
@@ -181,12 +182,18 @@ class Ffv1AviWriter:
                     self.stream.wait_event(ev)
                     src = FrameBatch.interleaved(self.fmt, self.w, self.h, n, device=self.device,
                                                  storage=self.stages[slot].storage[:n])
+                    import time
+                    t0 = time.perf_counter()
                     with torch.cuda.stream(self.stream):
                         data, sizes = self.enc.encode_host(src, stream=self.stream)
+                    t1 = time.perf_counter()
                     off = 0
                     for k in sizes.tolist():
                         self.avi.write_packet(data[off:off + k])
                         off += k
+                    self.stats["encode_s"] += t1 - t0
+                    self.stats["write_s"] += time.perf_counter() - t1
+                    self.stats["bytes"] += off
             except Exception as e:  # surfaced by the next write / close
                 self.err.append(e)
             finally:
@@ -275,7 +282,9 @@ class Ffv1AviReader:
     from the file when that batch is decoded, so a long-test AVPVS of tens of
     GB never sits in host memory."""
 
-    def __init__(self, path, batch=256, device=None):
+    def __init__(self, path, batch=600, device=None):
+        """batch: frames decoded per launch (the decoder's parallelism is
+        frames x slices, so a whole 10-s PVS at once)."""
         from . import avi
         info, self.index = avi.scan(path)
         if info.get("fourcc") != b"FFV1":
@@ -286,6 +295,7 @@ class Ffv1AviReader:
         self.fmt = self.dec.fmt
         self.pos = 0
         self.fh = open(path, "rb")
+        self._cache, self._cpos = None, 0  # decoded frames not yet handed out (read_device)
 
     @property
     def frame_bytes(self):
@@ -306,12 +316,32 @@ class Ffv1AviReader:
         return np.concatenate([span[o - lo:o - lo + s] for o, s in ent]), sizes
 
     def read_device(self, n):
-        """Decode up to n frames into an interleaved device FrameBatch (None at the end)."""
+        """Up to n decoded frames as an interleaved device FrameBatch (None at
+        the end).  Frames are decoded `batch` at a time into one device buffer
+        and handed out as views of it: a view is valid until the next call."""
+        from .frames import FrameBatch
+        if self._cache is None or self._cpos >= self._cache.n:
+            self._cache = self._decode(self.batch)
+            self._cpos = 0
+            if self._cache is None:
+                return None
+        k = min(n, self._cache.n - self._cpos)
+        out = FrameBatch.interleaved(self.fmt, self.w, self.h, k, device=self._cache.device,
+                                     storage=self._cache.storage[self._cpos:self._cpos + k])
+        self._cpos += k
+        return out
+
+    def _decode(self, n):
+        """Decode the next up to n packets into a (reused) device batch."""
         from .frames import FrameBatch
         k = min(n, len(self.index) - self.pos)
         if k <= 0:
             return None
-        out = FrameBatch.interleaved(self.fmt, self.w, self.h, k, device=torch.device("cuda", self.dec.ctx.device))
+        if getattr(self, "_dbuf", None) is None:
+            self._dbuf = FrameBatch.interleaved(self.fmt, self.w, self.h, self.batch,
+                                                device=torch.device("cuda", self.dec.ctx.device))
+        out = FrameBatch.interleaved(self.fmt, self.w, self.h, k, device=self._dbuf.device,
+                                     storage=self._dbuf.storage[:k])
         done = 0
         while done < k:
             m = min(self.batch, k - done)
@@ -325,12 +355,15 @@ class Ffv1AviReader:
 
     def read_into(self, buf, n):
         """Decode up to n frames into the dense host array buf [n, frame_bytes]; returns the count."""
-        out = self.read_device(n)
-        if out is None:
-            return 0
-        k = out.n
-        buf[:k] = out.storage[:k].cpu().numpy()
-        return k
+        done = 0
+        while done < n:
+            out = self.read_device(n - done)
+            if out is None:
+                break
+            k = out.n
+            buf[done:done + k] = out.storage[:k].cpu().numpy()
+            done += k
+        return done
 
     def close(self):
         self.fh.close()

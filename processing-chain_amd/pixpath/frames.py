@@ -45,8 +45,9 @@ class FrameBatch:
         bps = 1 if fm.packed else fm.bytes_per_sample
         base = flat.view(torch.uint16) if bps == 2 else flat
         planes, off = [], 0
+        so = base.storage_offset()  # as_strided's offset is absolute: keep a sliced storage's own
         for r, c in shapes:
-            planes.append(base.as_strided((n, r, c), (fb // bps, c, 1), off // bps))
+            planes.append(base.as_strided((n, r, c), (fb // bps, c, 1), so + off // bps))
             off += r * c * bps
         b = cls(fm, w, h, n, device=device, planes=planes)
         b.storage = storage

@@ -9,8 +9,10 @@ kernels and D2H of batch k.  H2D, compute and D2H are three HIP streams
 ordered by events only where a buffer is reused, so the two PCIe directions
 run concurrently (batch k+1's upload beside batch k-1's download) and both
 overlap the kernels.  A writer with ``write_device(batch, stream)`` takes the
-device output directly (the GPU FFV1 encoder): no D2H, no re-upload.  Frame
-layout everywhere is dense Y|U|V per frame.
+device output directly (the GPU FFV1 encoder): no D2H, no re-upload; a reader
+with ``read_device(n)`` hands over frames already in HBM (the GPU FFV1
+decoder): no host round trip, no H2D.  Frame layout everywhere is dense
+Y|U|V per frame.
 """
 import queue
 import threading
@@ -52,6 +54,8 @@ class Pipeline:
         """Stream all frames of `reader` through the stage into `writer`.
         ``emit(k_global, n)`` -> list of (batch-local index) to write for input frame k
         (fps maps duplicate / drop frames on the host); default: each frame once."""
+        if hasattr(reader, "read_device"):
+            return self._run_device_reader(reader, writer, emit)
         B = self.batch
         self.frames_in = self.frames_out = 0  # counts of this run
         rq = queue.Queue(maxsize=2)   # (slot, n) filled buffers
@@ -173,4 +177,57 @@ class Pipeline:
         tr.join(timeout=1.0)
         if err:
             raise err[0]
+        return self.frames_in
+
+    def _run_device_reader(self, reader, writer, emit):
+        """Frames come from the reader already in HBM (reader.read_device(n) ->
+        interleaved FrameBatch or None); the stage runs on them in place of the
+        H2D; outputs leave by D2H (or stay on the device for a device writer)."""
+        B = self.batch
+        self.frames_in = self.frames_out = 0
+        device_writer = hasattr(writer, "write_device")
+        base, slot = 0, 0
+        d2h_done = [None, None]
+        while True:
+            src = reader.read_device(B)
+            if src is None:
+                break
+            n = src.n
+            self.compute_stream.wait_stream(torch.cuda.current_stream(self.device))  # the decode's stream
+            if d2h_done[slot] is not None:
+                d2h_done[slot].synchronize()  # h_out[slot] / d_out[slot] are free again
+            with torch.cuda.stream(self.compute_stream):
+                dst = FrameBatch.interleaved(self.stage.out_fmt, self.stage.out_w, self.stage.out_h, n,
+                                             device=self.device, storage=self.d_out[slot].storage[:n])
+                self.stage.process(src, dst, self.compute_stream)
+            counts = None if emit is None else [emit(base + i) for i in range(n)]
+            if device_writer:
+                writer.write_device(dst, self.compute_stream, emit=counts)
+                ev = torch.cuda.Event()
+                ev.record(self.compute_stream)
+                d2h_done[slot] = ev
+            else:
+                with torch.cuda.stream(self.compute_stream):
+                    self.h_out[slot][:n].copy_(self.d_out[slot].storage[:n], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.compute_stream)
+                ev.synchronize()
+                buf = self.h_out[slot].numpy()
+                if counts is None:
+                    writer.write(buf[:n])
+                else:
+                    for i, c in enumerate(counts):
+                        for _ in range(c):
+                            writer.write(buf[i:i + 1])
+                d2h_done[slot] = None
+            self.frames_in += n
+            self.frames_out += n
+            base += n
+            slot ^= 1
+            # the reader may overwrite its device frames on the next call: the
+            # kernels that read them must be done
+            self.compute_stream.synchronize()
+            if n < B:
+                break
+        self.compute_stream.synchronize()
         return self.frames_in

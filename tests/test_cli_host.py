@@ -178,3 +178,17 @@ def test_gpu_backend_long_concat_string(tmp_path, monkeypatch):
         assert pff.create_avpvs_long_concat(pvs, overwrite=True).startswith("ffmpeg -nostdin -y -f concat")
     finally:
         pff.set_backend("ffmpeg")
+
+
+def test_interleaved_batch_on_a_storage_slice():
+    """FrameBatch.interleaved over rows k.. of another batch's storage views
+    those frames (as_strided's offset is absolute: the slice's own offset
+    must be kept) -- the FFV1 reader hands out such views."""
+    import torch
+    from pixpath.frames import FrameBatch
+    b = FrameBatch.interleaved("yuv422p10le", 16, 6, 4, device="cpu")
+    b.storage.copy_((torch.arange(b.storage.numel()) % 251).view_as(b.storage).to(torch.uint8))
+    for k in range(4):
+        v = FrameBatch.interleaved("yuv422p10le", 16, 6, 4 - k, device="cpu", storage=b.storage[k:])
+        for p in range(3):
+            assert torch.equal(v.view(p)[0], b.view(p)[k])

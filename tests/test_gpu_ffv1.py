@@ -19,6 +19,51 @@ CASES = [("yuv422p10le", po.YUV422P10LE, 10, 1, 0), ("yuv420p", po.YUV420P, 8, 1
          ("yuv420p10le", po.YUV420P10LE, 10, 1, 1), ("yuv422p", po.YUV422P, 8, 1, 0)]
 
 
+def _const_frame(fid, w, h, v):
+    depth, hs, vs = po.fmt_info(fid)
+    dt = np.uint16 if depth > 8 else np.uint8
+    return [np.full(sh, v << (depth - 8), dt) for sh in po.plane_shapes(fid, w, h)]
+
+
+def _gradient_frame(fid, w, h, t, rng):
+    """bench.py --workload ffv1 content: moving gradients + noise in [-4, 4]."""
+    depth, hs, vs = po.fmt_info(fid)
+    dt = np.uint16 if depth > 8 else np.uint8
+    hi = (1 << depth) - 1
+    out = []
+    for p, (r, c) in enumerate(po.plane_shapes(fid, w, h)):
+        yy, xx = np.mgrid[0:r, 0:c]
+        v = (xx * (p + 1) + yy * 2 + 3 * t) % (hi * 4 // 5) + hi // 10 + rng.integers(-4, 5, (r, c))
+        out.append(np.clip(v, 0, hi).astype(dt))
+    return out
+
+
+@pytest.mark.parametrize("name,fid,bits,hs,vs", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("grid", [(8, 8), (16, 16)])
+def test_gpu_constant_and_gradient_content(gpu, name, fid, bits, hs, vs, grid):
+    """Content with very few contexts (a constant frame: tiny slices, the
+    |residual| = 2^(bits-1) border samples) and the bench's moving gradients:
+    GPU packets byte-identical to the C restatement, and the GPU decoder
+    returns the input from both its own and the restatement's packets."""
+    from pixpath import ffv1
+    w, h = 1920, 1080
+    rng = np.random.default_rng(bits + grid[0])
+    frames = [_const_frame(fid, w, h, 128), _gradient_frame(fid, w, h, 3, rng)]
+    enc = ffv1.Ffv1Encoder(name, w, h, slices=grid, max_frames=len(frames), device=gpu)
+    pkts = enc.encode_to_host(_batch(gpu, name, frames))
+    dec = ffv1.Ffv1Decoder(enc.extradata, w, h, max_frames=len(frames), device=gpu)
+    for f, planes in enumerate(frames):
+        want = ref.encode_frame(planes, bits, hs, vs, *grid)
+        if pkts[f] != want:
+            n = min(len(pkts[f]), len(want))
+            first = next((i for i in range(n) if pkts[f][i] != want[i]), n)
+            pytest.fail("frame %d: %d vs %d bytes, first difference at %d" % (f, len(pkts[f]), len(want), first))
+        for pk in (pkts[f], want):
+            out = dec.decode(pk, [len(pk)]).to_numpy()
+            for p in range(3):
+                np.testing.assert_array_equal(out[p][0], planes[p])
+
+
 def _batch(gpu, name, frames):
     from pixpath.frames import FrameBatch
     return FrameBatch.from_numpy(name, [np.stack([f[p] for f in frames]) for p in range(3)], device=gpu)
