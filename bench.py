@@ -313,15 +313,21 @@ def pcie_pipeline(wl, n_frames, dev):
                     "host fill of the pinned input is included, decode/encode are not"}
 
 
-def e2e_avpvs(wl, n_frames, dev):
+def e2e_avpvs(wl, n_frames, dev, n_pvs=4):
     """The product path of `cli avpvs --gpu-ffv1` end to end (SURVEY.md 8d's
     third row): dense host frames -> pinned batches -> H2D -> strip_kernel ->
     FFV1 encode of the DEVICE output (no D2H of pixels) -> packets D2H -> AVI
     bytes written to a file.  Host decode is replaced by a memory reader of
     compressible synthetic frames (moving gradients + noise: FFV1 codes them
     at ~4:1, like upscaled video); the rate includes the reader's copies and
-    the file writes.  Never `value`."""
+    the file writes.  Several PVSes in a row, as the reference's ParallelRunner
+    feeds them (lib/cmd_utils.py:93-101): each writer encodes and writes its
+    PVS on its own worker thread and stream while the next PVS is scaled, so
+    the scale, encode and file-write stages of consecutive PVSes overlap.
+    `single_pvs` is the same path for one PVS with nothing to overlap.  Never
+    `value`."""
     import tempfile
+    import threading
     import numpy as np
     import torch
     from pixpath import formats, ops
@@ -355,28 +361,55 @@ def e2e_avpvs(wl, n_frames, dev):
     stage = Stage(sfmt, sw, sh, dfmt, dw, dh, lambda s, d, st: sc(s, d, stream=st))
     pl = Pipeline(stage, batch=60, device=dev.index)
     d = tempfile.mkdtemp(prefix="pixpath_e2e_")
-    path = os.path.join(d, "PVS.avi")
+    paths = [os.path.join(d, "PVS%d.avi" % k) for k in range(n_pvs)]
+
+    def run(count):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        closers, errs, stats, n = [], [], [], 0
+
+        def close(wr):  # encode + write of PVS k overlap the scale of PVS k + 1
+            try:
+                wr.close()
+                stats.append(dict(wr.stats))
+            except Exception as e:  # re-raised below
+                errs.append(e)
+            wr.release()
+        for k in range(count):
+            wr = Ffv1AviWriter(paths[k], dfmt, dw, dh, 60, slices=(8, 8), batch=n_frames, device=dev.index)
+            n += pl.run(MemReader(), wr)
+            th = threading.Thread(target=close, args=(wr,))
+            th.start()
+            closers.append(th)
+            del wr
+        for th in closers:
+            th.join()
+        dt = time.perf_counter() - t0
+        if errs:
+            raise errs[0]
+        return n, dt, stats
+
     try:
-        for rep in range(2):  # the first pass warms the encoder (allocations, kernel loads)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            wr = Ffv1AviWriter(path, dfmt, dw, dh, 60, slices=(8, 8), batch=n_frames, device=dev.index)
-            n = pl.run(MemReader(), wr)
-            t_pipe = time.perf_counter() - t0
-            wr.close()
-            dt = time.perf_counter() - t0
-        size = os.path.getsize(path)
+        run(1)  # warm-up (allocations, kernel loads)
+        n1, dt1, w1 = run(1)
+        size = os.path.getsize(paths[0])
+        n, dt, ws = run(n_pvs)
     finally:
-        if os.path.exists(path):
-            os.remove(path)
+        for p_ in paths:
+            if os.path.exists(p_):
+                os.remove(p_)
         os.rmdir(d)
-    return {"frames_per_s": round(n / dt, 1), "frames": n, "seconds": round(dt, 3), "avi_bytes": size,
-            "breakdown_s": {"host_to_scaled_in_hbm": round(t_pipe, 3), "ffv1_encode_and_d2h": round(wr.stats["encode_s"], 3),
-                            "avi_write": round(wr.stats["write_s"], 3)},
-            "compression": round(n * frame_bytes(dfmt, dw, dh) / size, 3),
-            "note": "host frames -> pinned batches of 60 -> H2D -> strip_kernel (720p->1080p yuv422p10le lanczos) "
-                    "-> FFV1 v3 encode on the device output (8x8 slices, one 600-frame batch) -> packets D2H -> "
-                    "AVI file; decode of the SRC bitstream excluded (ffmpeg is absent on the box)"}
+    st = w1[0]
+    return {"frames_per_s": round(n / dt, 1), "frames": n, "pvs": n_pvs, "seconds": round(dt, 3),
+            "single_pvs": {"frames_per_s": round(n1 / dt1, 1), "seconds": round(dt1, 3),
+                           "breakdown_s": {"ffv1_encode_and_d2h": round(st["encode_s"], 3),
+                                           "avi_write": round(st["write_s"], 3)}},
+            "avi_bytes_per_pvs": size, "compression": round(n1 * frame_bytes(dfmt, dw, dh) / size, 3),
+            "note": "%d PVSes of %d frames: host frames -> pinned batches of 60 -> H2D -> strip_kernel "
+                    "(720p->1080p yuv422p10le lanczos) -> FFV1 v3 encode on the device output (8x8 slices, one "
+                    "batch per PVS, the writer's worker thread and stream) -> packets D2H -> AVI file; consecutive "
+                    "PVSes overlap; decode of the SRC bitstream excluded (ffmpeg is absent on the box)"
+                    % (n_pvs, n_frames)}
 
 
 def make_inputs(wl, n, seed, dev):

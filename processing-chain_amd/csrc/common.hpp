@@ -7,6 +7,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -53,6 +54,21 @@ inline FmtInfo fmt_info(int f) {
 }
 
 inline int ceil_rshift(int a, int s) { return -((-a) >> s); }
+
+// FFV1 coder / decoder: slices (active lanes) per 64-lane wave.  The range
+// coder of a slice is one serial chain and a 600-frame batch has only
+// frames x slices chains; fewer lanes per wave trade issue slots for waves.
+// Measured (profiles/r3): the encoder's coder is issue-bound per wave (full
+// waves best), the decoder waits on its context-block loads (32 lanes best).
+// PIXPATH_FFV1_LPW overrides both (1..64).
+inline int ffv1_lanes_per_wave(int dflt) {
+    static const int v = [] {
+        const char *e = std::getenv("PIXPATH_FFV1_LPW");
+        const int x = e ? std::atoi(e) : 0;
+        return x >= 1 && x <= 64 ? x : 0;
+    }();
+    return v ? v : dflt;
+}
 
 // MI355X dispatches the workgroups of a 1-D grid round-robin over its 8 XCDs
 // (block b -> XCD b % 8), each with its own L2.  Remapping hardware block `b`

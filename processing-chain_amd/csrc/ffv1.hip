@@ -11,12 +11,11 @@
 // unit of parallelism is the slice: ONE LANE PER SLICE, every slice of every
 // frame of the batch at once (600 frames x 64 slices = 38,400 lanes).  Only
 // the coder itself is serial, so the encode is split in four launches:
-//   ffv1_model_kernel   data-parallel, one thread per slice-plane row: the
-//                       context (quantised L-TL, TL-T, T-TR) and the folded
+//   ffv1_model_kernel   data-parallel, one thread per token: the context
+//                       (quantised L-TL, TL-T, T-TR) and the folded
 //                       median-prediction residual of every sample, as one
 //                       32-bit token, laid out [wave group][sample][lane] so
-//                       the coder's 64 lanes read one coalesced 256-B line per
-//                       sample;
+//                       the coder's lanes read one coalesced line per sample;
 //   ffv1_code_kernel    one lane per slice: put_symbol on the token stream.  The
 //                       32 state bytes of the current context live in 8 VGPRs;
 //                       the tokens are known in advance, so the state block of
@@ -169,6 +168,7 @@ struct Ffv1Args {
     uint32_t *raw;          // [nslices][raw_cap] renorm records, two per dword
     int64_t raw_cap;        // dwords per slice
     int32_t *nraw;          // [nslices] records, -1 = overflow
+    int lpw;                // slices (active lanes) per 64-lane coder workgroup
 };
 
 __device__ inline int dquant(int d) {  // d already & 0xFF
@@ -271,80 +271,88 @@ __device__ __host__ inline SliceGeo slice_geo(int g, int w, int h, int nh, int n
 }
 
 // ---- 1. modelling: tokens (context key << 16 | folded residual) -------------
-// One workgroup per (64-slice wave group, plane row); 64 threads = the coder
-// wave's 64 lanes.  The row and the row above of all 64 slices are staged in
-// LDS 64 columns at a time with coalesced loads (consecutive threads read
-// consecutive samples of one slice row), then each thread walks its own
-// slice's columns from LDS and stores one token per column -- the 64 threads'
-// stores of a column are one contiguous 256-B line.  key = plane set * 666 +
-// |context|; the residual is negated with the context (encode_line), folded
-// to the bit depth, stored as int16.
+// One workgroup of 256 threads per (64-slice wave group, plane row).  A token
+// depends only on input samples (L = cur[x-1], T / TL / TR from the row
+// above; FFmpeg's borders at the slice edges), so every token is independent:
+// the row and the row above of the 64 slices are staged in LDS kMX columns at
+// a time (consecutive threads read consecutive samples of one slice row:
+// coalesced), then thread (lane = t & 63, column phase = t >> 6) computes the
+// tokens of its lane at columns phase, phase + 4, ... and the 64 threads of a
+// wave store one token column as one contiguous 256-B line
+// ([wave group][sample][lane], the coder's layout).  Lanes of one workgroup
+// can be in different planes (slices of unequal height), so every row pointer
+// and width is per lane.  key = plane set * 666 + |context|; the residual is
+// negated with the context (encode_line), folded to the bit depth, int16.
 constexpr int kMX = 64;          // columns per staged chunk
-constexpr int kMS = kMX + 3;     // staged samples per row: x0 - 1 .. x0 + 64 (+1); odd stride, no bank conflicts
+constexpr int kMS = kMX + 2;     // staged samples per row: x0 - 1 .. x0 + 64
+constexpr int kMLane = 2 * kMS + 1;  // lane stride in LDS (odd: no bank conflicts)
 template <typename ST>
-__global__ __launch_bounds__(64) void ffv1_model_kernel(const Ffv1Args a) {
-    __shared__ int s_row[64][2][kMS];  // [lane][top, cur][column x0 - 1 + j]
+__global__ __launch_bounds__(256) void ffv1_model_kernel(const Ffv1Args a) {
+    __shared__ int s_row[64 * kMLane];        // [lane][top, cur][column x0 - 1 + j]
+    __shared__ uint64_t s_ptr[64][2];         // [lane][row above, row]
+    __shared__ int s_info[64][5];             // pw, has-T, TL0, token offset, context key base
     const int t = threadIdx.x;
     const int wg = blockIdx.y;
-    const int g = wg * 64 + t;
-    const bool live = g < a.nslices;
-    const SliceGeo q = slice_geo(live ? g : 0, a.w, a.h, a.nh, a.nv, a.hsub, a.vsub);
-    int r = blockIdx.x, p = 0, off = 0;
-    bool on = live;
-    if (r < q.lh) {
-        p = 0;
-    } else if ((r -= q.lh) < q.ch) {
-        p = 1; off = q.lw * q.lh;
-    } else if ((r -= q.ch) < q.ch) {
-        p = 2; off = q.lw * q.lh + q.cw * q.ch;
-    } else {
-        on = false;
+    if (t < 64) {
+        const int g = wg * 64 + t;
+        const bool live = g < a.nslices;
+        const SliceGeo q = slice_geo(live ? g : 0, a.w, a.h, a.nh, a.nv, a.hsub, a.vsub);
+        int r = blockIdx.x, p = 0, off = 0;
+        bool on = live;
+        if (r < q.lh) {
+            p = 0;
+        } else if ((r -= q.lh) < q.ch) {
+            p = 1; off = q.lw * q.lh;
+        } else if ((r -= q.ch) < q.ch) {
+            p = 2; off = q.lw * q.lh + q.cw * q.ch;
+        } else {
+            on = false;
+        }
+        const int y = r;
+        const int pw = on ? (p ? q.cw : q.lw) : 0;
+        const int px0 = p ? q.x0 >> a.hsub : q.x0, py0 = p ? q.y0 >> a.vsub : q.y0;
+        const uint8_t *src = p == 0 ? a.src[0] : p == 1 ? a.src[1] : a.src[2];
+        const int64_t ls = p == 0 ? a.ls[0] : p == 1 ? a.ls[1] : a.ls[2];
+        const int64_t fs = p == 0 ? a.fs[0] : p == 1 ? a.fs[1] : a.fs[2];
+        const uint8_t *rowb = on ? src + q.frame * fs + (int64_t)(py0 + y) * ls + (int64_t)px0 * sizeof(ST) : src;
+        s_ptr[t][0] = reinterpret_cast<uint64_t>(rowb - ls);
+        s_ptr[t][1] = reinterpret_cast<uint64_t>(rowb);
+        s_info[t][0] = pw;
+        s_info[t][1] = on && y > 0;
+        // FFmpeg's sample-buffer borders: 0 above the slice, L = T at column 0,
+        // TL at column 0 = first sample two rows up, TR past the last column = T
+        s_info[t][2] = on && y > 1 ? reinterpret_cast<const ST *>(rowb - 2 * ls)[0] : 0;
+        s_info[t][3] = off + y * pw;
+        s_info[t][4] = p ? kFfv1Ctx : 0;
     }
-    const int y = r;
-    const int pw = on ? (p ? q.cw : q.lw) : 0;
-    const int px0 = p ? q.x0 >> a.hsub : q.x0, py0 = p ? q.y0 >> a.vsub : q.y0;
-    const uint8_t *src = p == 0 ? a.src[0] : p == 1 ? a.src[1] : a.src[2];
-    const int64_t ls = p == 0 ? a.ls[0] : p == 1 ? a.ls[1] : a.ls[2];
-    const int64_t fs = p == 0 ? a.fs[0] : p == 1 ? a.fs[1] : a.fs[2];
-    // this lane's row start; broadcast per staged slice with readlane
-    const uint8_t *rowb = on ? src + q.frame * fs + (int64_t)(py0 + y) * ls + (int64_t)px0 * sizeof(ST) : src;
-    const uint64_t rowv = reinterpret_cast<uint64_t>(rowb);
-    const int hasT = on && y > 0;
+    __syncthreads();
+    const int lane = t & 63, ph = t >> 6;
+    const int pw = s_info[lane][0], TL0 = s_info[lane][2];
     const int mask = (1 << a.bits) - 1, half = 1 << (a.bits - 1);
-    const uint32_t key0 = p ? kFfv1Ctx : 0;
-    uint32_t *out = a.tok + ((int64_t)wg * a.tok_len + off + (int64_t)y * pw) * 64 + t;
-    // FFmpeg's sample-buffer borders: 0 above the slice, L = T at column 0,
-    // TL at column 0 = first sample two rows up, TR past the last column = T
-    const int TL0 = on && y > 1 ? reinterpret_cast<const ST *>(rowb - 2 * ls)[0] : 0;
-    int pw_max = pw;
-    for (int o = 32; o > 0; o >>= 1) pw_max = max(pw_max, __shfl_xor(pw_max, o));
-    int L = 0, TL = 0;
+    uint32_t *out = a.tok + ((int64_t)wg * a.tok_len + s_info[lane][3]) * 64 + lane;
+    const uint32_t kbase = (uint32_t)s_info[lane][4];
+    int pw_max = 0;
+    for (int j = 0; j < 64; ++j) pw_max = max(pw_max, s_info[j][0]);
+    int *const my = s_row + lane * kMLane;
     for (int x0 = 0; x0 < pw_max; x0 += kMX) {
-        __syncthreads();  // the previous chunk's LDS reads are done
-        // stage columns x0 - 1 .. x0 + 65 of the row and the row above of every slice
-        for (int j = 0; j < 64; ++j) {
-            const uint64_t rb = ((uint64_t)__builtin_amdgcn_readlane((int)(rowv >> 32), j) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rowv, j);
-            const int pwj = __builtin_amdgcn_readlane(pw, j), tj = __builtin_amdgcn_readlane(hasT, j);
-            const ST *rr = reinterpret_cast<const ST *>(rb);
-            for (int e = t; e < 2 * kMS; e += 64) {
-                const int rw = e >= kMS ? 1 : 0, col = e - rw * kMS, x = x0 - 1 + col;
-                int v = 0;
-                if (x >= 0 && x < pwj && (rw || tj)) v = rw ? rr[x] : reinterpret_cast<const ST *>(rb - ls)[x];
-                s_row[j][rw][col] = v;
-            }
+        if (x0) __syncthreads();  // the previous chunk's LDS reads are done
+        // stage columns x0 - 1 .. x0 + 64 of the row above and the row of every lane
+        for (int e = t; e < 64 * 2 * kMS; e += 256) {
+            const int j = e / (2 * kMS), rem = e - j * (2 * kMS);
+            const int rw = rem >= kMS ? 1 : 0, col = rem - rw * kMS, x = x0 - 1 + col;
+            int v = 0;
+            if (x >= 0 && x < s_info[j][0] && (rw || s_info[j][1]))
+                v = reinterpret_cast<const ST *>(s_ptr[j][rw])[x];
+            s_row[j * kMLane + rw * kMS + col] = v;
         }
         __syncthreads();
         const int xe = min(pw, x0 + kMX);
-        for (int x = x0; x < xe; ++x) {
+        for (int x = x0 + ph; x < xe; x += 4) {
             const int c = x - x0 + 1;
-            const int T = s_row[t][0][c];
-            const int v = s_row[t][1][c];
-            if (x == 0) {
-                L = T;
-                TL = TL0;
-            }
-            const int TR = x + 1 < pw ? s_row[t][0][c + 1] : T;
+            const int T = my[c], v = my[kMS + c];
+            const int L = x ? my[kMS + c - 1] : T;
+            const int TL = x ? my[c - 1] : TL0;
+            const int TR = x + 1 < pw ? my[c + 1] : T;
             int ctx = dquant((L - TL) & 0xFF) + 11 * dquant((TL - T) & 0xFF) + 121 * dquant((T - TR) & 0xFF);
             int diff = v - median3(L, L + T - TL, T);
             if (ctx < 0) {
@@ -353,49 +361,62 @@ __global__ __launch_bounds__(64) void ffv1_model_kernel(const Ffv1Args a) {
             }
             diff &= mask;
             diff = diff >= half ? diff - (mask + 1) : diff;
-            out[(int64_t)x * 64] = ((key0 + (uint32_t)ctx) << 16) | ((uint32_t)diff & 0xFFFFu);
-            L = v;
-            TL = T;
+            out[(int64_t)x * 64] = ((kbase + (uint32_t)ctx) << 16) | ((uint32_t)diff & 0xFFFFu);
         }
     }
 }
 
 // ---- 2. coding ---------------------------------------------------------------
-// The range coder of one lane.  renorm records, per output byte,
-// (low >> 8) | ((low & 0xFF) == 0) << 9 as a 16-bit value in the lane's LDS
-// ring; ffv1_resolve_kernel turns them into bytes exactly as renorm_encoder
-// does.  Every coding step ends with one unconditional store of the ring's
-// oldest 16 records, so the number of vector-memory operations per step is a
-// constant and the wait for a block loaded two steps earlier can leave the
-// younger loads and stores in flight (vmcnt counts both, in order).
-constexpr int kRing = 64;    // records per lane ring (LDS)
-constexpr int kFlush = 16;   // records stored per step (2 x 16 B)
+// The range coder of one lane.  A lane's decisions are the wave's work unit:
+// the 64 lanes of a wave code different slices, so a symbol costs the wave the
+// LONGEST symbol among its lanes.  Every decision is therefore branch-free
+// (a lane whose symbol is shorter codes no-op decisions: state 0, bit 0 leaves
+// low / range unchanged), and the wave-uniform exponent bound E (four ballots)
+// skips the decision slots no lane needs with scalar branches.
+// Renormalisation records `low` (before the shift) per output byte in the
+// lane's LDS ring with an unconditional store at the write position (a
+// decision that does not renormalise leaves the position, so the next one
+// overwrites it); the ring leaves kFlush records per 4 samples, packed to 16 bits
+// ((low >> 8) | ((low & 0xFF) == 0) << 9), and ffv1_resolve_kernel turns them
+// into bytes exactly as renorm_encoder does.  The 4 unrolled coding steps
+// issue a fixed pattern of vector-memory operations (token load, block load,
+// block store per step, the record store in the fourth), so the wait for a
+// block loaded two steps earlier can leave the younger loads and stores in
+// flight (vmcnt counts both, in order).
+constexpr int kRing = 128;   // records per lane ring (LDS, u32)
+// lane stride of the rings: odd, so the 64 lanes' stores at similar write
+// positions fall in different LDS banks (a 128-dword stride put every lane's
+// record store of a decision in the same bank: a 64-way conflict per decision)
+constexpr int kRingStride = kRing + 1;
+constexpr int kFlush = 16;   // records stored per flush (32 B), one flush per 4 samples
 struct Enc {
     uint32_t low, range;
-    uint16_t *ring;          // this lane's kRing records
+    uint32_t *ring;          // this lane's kRing records
     uint32_t wp;             // records pushed
 };
 
-__device__ __forceinline__ void enc_renorm(Enc &c) {
-    if (c.range < 0x100u) {
-        const uint32_t raw = (c.low >> 8) | ((c.low & 0xFFu) == 0u ? 0x200u : 0u);
-        c.ring[c.wp & (kRing - 1)] = (uint16_t)raw;
-        ++c.wp;
-        c.low = (c.low & 0xFFu) << 8;
-        c.range <<= 8;
-    }
-}
-
-// one binary decision with state value s; returns the next state (LDS table
-// lookup: zero[] at 0, one[] at 256), which the caller writes back later
-__device__ __forceinline__ uint32_t enc_rac(Enc &c, uint32_t s, uint32_t bit, const uint8_t *tab) {
+// one binary decision (put_rac) with state value s, branch-free; s = 0 and
+// bit = 0 is a no-op (r1 = 0: low and range stay, range >= 0x100: no renorm)
+__device__ __forceinline__ void enc_dec(Enc &c, uint32_t s, bool bit) {
     const uint32_t r1 = __umul24(c.range, s) >> 8;
     const uint32_t rz = c.range - r1;
     c.low += bit ? rz : 0u;
     c.range = bit ? r1 : rz;
-    const uint32_t ns = tab[s | (bit << 8)];
-    enc_renorm(c);
-    return ns;
+    c.ring[c.wp & (kRing - 1)] = c.low;
+    const bool rn = c.range < 0x100u;
+    c.wp += rn ? 1u : 0u;
+    c.low = rn ? (c.low << 8) & 0xFF00u : c.low;
+    c.range = rn ? c.range << 8 : c.range;
+}
+
+// renorm_encoder for the terminating flushes (outside the hot loop)
+__device__ __forceinline__ void enc_renorm(Enc &c) {
+    if (c.range < 0x100u) {
+        c.ring[c.wp & (kRing - 1)] = c.low;
+        ++c.wp;
+        c.low = (c.low & 0xFFu) << 8;
+        c.range <<= 8;
+    }
 }
 
 // state byte k of a 32-byte block held in 8 dwords (k a compile-time constant
@@ -404,50 +425,77 @@ __device__ __forceinline__ uint32_t sget(const uint32_t (&b)[8], int k) { return
 __device__ __forceinline__ void sput(uint32_t (&b)[8], int k, uint32_t v) {
     b[k >> 2] = (b[k >> 2] & ~(0xFFu << ((k & 3) * 8))) | (v << ((k & 3) * 8));
 }
-// runtime index k in 8..23 (the sign state 11 + e)
+// runtime index k in 8..23 (the sign state 11 + e), branch-free selects
 __device__ __forceinline__ uint32_t sget_dyn(const uint32_t (&b)[8], int k) {
     const int w = k >> 2;
-    const uint32_t x = w == 2 ? b[2] : w == 3 ? b[3] : w == 4 ? b[4] : b[5];
-    return (x >> ((k & 3) * 8)) & 0xFFu;
+    const uint32_t lo = (w & 1) ? b[3] : b[2], hi = (w & 1) ? b[5] : b[4];
+    return __builtin_amdgcn_ubfe(w >= 4 ? hi : lo, (k & 3) * 8, 8);
 }
-__device__ __forceinline__ void sput_dyn(uint32_t (&b)[8], int k, uint32_t v) {
+__device__ __forceinline__ void sput_dyn(uint32_t (&b)[8], int k, uint32_t v, bool on) {
     const int w = k >> 2;
     const uint32_t sh = (k & 3) * 8, m = ~(0xFFu << sh), nv = v << sh;
-    b[2] = w == 2 ? (b[2] & m) | nv : b[2];
-    b[3] = w == 3 ? (b[3] & m) | nv : b[3];
-    b[4] = w == 4 ? (b[4] & m) | nv : b[4];
-    b[5] = w == 5 ? (b[5] & m) | nv : b[5];
+    b[2] = on && w == 2 ? (b[2] & m) | nv : b[2];
+    b[3] = on && w == 3 ? (b[3] & m) | nv : b[3];
+    b[4] = on && w == 4 ? (b[4] & m) | nv : b[4];
+    b[5] = on && w == 5 ? (b[5] & m) | nv : b[5];
+}
+
+// wave-uniform max of e over the live lanes (e in -1..15): a binary search of ballots
+__device__ __forceinline__ int wave_max_e(int e) {
+    int E = -1;
+    if (__builtin_amdgcn_ballot_w64(e >= E + 8)) E += 8;
+    if (__builtin_amdgcn_ballot_w64(e >= E + 4)) E += 4;
+    if (__builtin_amdgcn_ballot_w64(e >= E + 2)) E += 2;
+    if (__builtin_amdgcn_ballot_w64(e >= E + 1)) E += 1;
+    return __builtin_amdgcn_readfirstlane(E);
 }
 
 // put_symbol (ffv1enc.c put_symbol_inline) on a register block, |v| < 1024:
-// every state byte the symbol uses is read from `b` before the first
-// decision and the updated bytes are written after the last one.
+// every state byte the symbol uses is read from `b` before the first decision
+// (each is used at most once per symbol), the next states come from the LDS
+// tables in one batch of reads (they depend on the bits only, not on low /
+// range), and the updated bytes are written after the last decision.
 template <bool SIGNED>
 __device__ __forceinline__ void enc_symbol(Enc &c, uint32_t (&b)[8], int v, const uint8_t *tab) {
     const uint32_t a = (uint32_t)(v < 0 ? -v : v);
     const bool nz = v != 0;
-    const int e = nz ? 31 - __clz(a) : 0;
-    const uint32_t n0 = enc_rac(c, sget(b, 0), nz ? 0u : 1u, tab);
-    uint32_t nu[10], nm[9], nsg = 0;
-    if (nz) {
+    const int e = nz ? 31 - __clz(a) : -1;
+    const int E = wave_max_e(e);
+    const uint32_t s0 = sget(b, 0);
+    uint32_t su[10], sm[9], ss = 0, n0, nu[10], nm[9], nsg = 0;
+    n0 = tab[s0 | (nz ? 0u : 256u)];
 #pragma unroll
-        for (int i = 0; i < 10; ++i)
-            if (i <= e) nu[i] = enc_rac(c, sget(b, 1 + i), i < e ? 1u : 0u, tab);
+    for (int i = 0; i < 10; ++i)
+        if (i <= E) {
+            su[i] = sget(b, 1 + i);
+            nu[i] = tab[su[i] | (i < e ? 256u : 0u)];
+        }
 #pragma unroll
-        for (int i = 8; i >= 0; --i)
-            if (i < e) nm[i] = enc_rac(c, sget(b, 22 + i), (a >> i) & 1u, tab);
-        if constexpr (SIGNED) nsg = enc_rac(c, sget_dyn(b, 11 + e), v < 0 ? 1u : 0u, tab);
+    for (int i = 0; i < 9; ++i)
+        if (i < E) {
+            sm[i] = sget(b, 22 + i);
+            nm[i] = tab[sm[i] | (((a >> i) & 1u) << 8)];
+        }
+    if (SIGNED && E >= 0) {
+        ss = sget_dyn(b, 11 + (e < 0 ? 0 : e));
+        nsg = tab[ss | (v < 0 ? 256u : 0u)];
     }
+    enc_dec(c, s0, !nz);
+#pragma unroll
+    for (int i = 0; i < 10; ++i)
+        if (i <= E) enc_dec(c, i <= e ? su[i] : 0u, i < e);
+#pragma unroll
+    for (int i = 8; i >= 0; --i)
+        if (i < E) enc_dec(c, i < e ? sm[i] : 0u, i < e && ((a >> i) & 1u));
+    if (SIGNED && E >= 0) enc_dec(c, nz ? ss : 0u, v < 0);
     sput(b, 0, n0);
-    if (nz) {
 #pragma unroll
-        for (int i = 0; i < 10; ++i)
-            if (i <= e) sput(b, 1 + i, nu[i]);
+    for (int i = 0; i < 10; ++i)
+        if (i <= E) sput(b, 1 + i, i <= e ? nu[i] : su[i]);
 #pragma unroll
-        for (int i = 0; i < 9; ++i)
-            if (i < e) sput(b, 22 + i, nm[i]);
-        if constexpr (SIGNED) sput_dyn(b, 11 + e, nsg);
-    }
+    for (int i = 0; i < 9; ++i)
+        if (i < E) sput(b, 22 + i, i < e ? nm[i] : sm[i]);
+    if (SIGNED && E >= 0) sput_dyn(b, 11 + (e < 0 ? 0 : e), nsg, nz);
 }
 
 __device__ __forceinline__ void blk_load(uint32_t (&b)[8], const uint8_t *p) {
@@ -463,47 +511,63 @@ __device__ __forceinline__ void blk_sel(uint32_t (&d)[8], bool c, const uint32_t
     for (int i = 0; i < 8; ++i) d[i] = c ? x[i] : y[i];
 }
 
+// 16-bit renorm record of a recorded `low`: low >> 8 (9 bits) | exact << 9
+__device__ __forceinline__ uint32_t rec16(uint32_t low) { return (low >> 8) | ((low & 0xFFu) == 0u ? 0x200u : 0u); }
+
 __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
     __shared__ uint8_t s_tab[512];  // zero[256], one[256]
-    __shared__ __align__(16) uint16_t s_ring[64 * kRing];
+    __shared__ __align__(16) uint32_t s_ring[64 * kRingStride];
     for (int i = threadIdx.x; i < 512; i += 64) s_tab[i] = a.tables[i];
     __syncthreads();
     const int lane = threadIdx.x;
-    const int g = blockIdx.x * 64 + lane;
+    if (lane >= a.lpw) return;
+    const int g = blockIdx.x * a.lpw + lane;
     if (g >= a.nslices) return;
     const SliceGeo q = slice_geo(g, a.w, a.h, a.nh, a.nv, a.hsub, a.vsub);
     const int len = q.len();
     uint8_t *const st0 = a.states + (int64_t)g * kStateBytes;
-    const uint32_t *tp = a.tok + (int64_t)blockIdx.x * a.tok_len * 64 + lane;
+    // tokens of slice g: group g / 64 of the modelling layout, lane g % 64
+    const uint32_t *tp = a.tok + (int64_t)(g >> 6) * a.tok_len * 64 + (g & 63);
     Enc c;
     c.low = 0; c.range = 0xFF00; c.wp = 0;
-    c.ring = s_ring + lane * kRing;
-    // records leave the ring kFlush at a time into the lane's record buffer;
-    // `fp` records are final there, the rest of the 16 is rewritten next step
-    uint8_t *const out = reinterpret_cast<uint8_t *>(a.raw + (int64_t)g * a.raw_cap);
+    c.ring = s_ring + lane * kRingStride;
+    // records leave the ring kFlush at a time (packed to 16 bits) into the
+    // lane's record buffer; `fp` records are final there, the rest of the
+    // kFlush is rewritten next step
+    uint16_t *const out = reinterpret_cast<uint16_t *>(a.raw + (int64_t)g * a.raw_cap);
     const uint32_t cap = (uint32_t)(a.raw_cap * 2) & ~(uint32_t)(kFlush - 1);  // records the buffer holds
     uint32_t fp = 0;
     bool over = false;
     auto flush = [&]() {
-        const uint4 *r = reinterpret_cast<const uint4 *>(c.ring + (fp & (kRing - 1)));
-        const uint4 x = r[0], y = r[1];
-        uint4 *d = reinterpret_cast<uint4 *>(out + 2 * (int64_t)(fp < cap ? fp : cap - kFlush));
-        d[0] = x;
-        d[1] = y;
-        over |= c.wp - fp > (uint32_t)(kRing - kFlush) || fp >= cap;
+        const uint32_t *r = c.ring + (fp & (kRing - 1));  // dword reads (the lane stride is odd)
+        uint4 *d = reinterpret_cast<uint4 *>(out + (fp < cap ? fp : cap - kFlush));
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint4 pk;
+            pk.x = rec16(r[8 * h + 0]) | (rec16(r[8 * h + 1]) << 16);
+            pk.y = rec16(r[8 * h + 2]) | (rec16(r[8 * h + 3]) << 16);
+            pk.z = rec16(r[8 * h + 4]) | (rec16(r[8 * h + 5]) << 16);
+            pk.w = rec16(r[8 * h + 6]) | (rec16(r[8 * h + 7]) << 16);
+            d[h] = pk;
+        }
+        // the next 4 samples add at most 4 x 22 records: the ring must keep room for them
+        over |= c.wp - fp > (uint32_t)(kRing - 88 + kFlush) || fp >= cap;
         if (c.wp - fp >= (uint32_t)kFlush) fp += kFlush;
     };
     // keyframe bit (first slice of a frame), then the slice header with its own 32 states:
     // slice x, y, width - 1, height - 1 (slice units), table set of Y and of Cb/Cr,
     // picture_structure 3 (progressive), SAR 1:1 (setsar=1/1)
-    if (q.s == 0) (void)enc_rac(c, 128, 1, s_tab);
+    if (q.s == 0) enc_dec(c, 128, true);
     {
         uint32_t hb[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) hb[i] = 0x80808080u;
         const int hv[9] = {q.sx, q.sy, 0, 0, 0, 0, 3, 1, 1};
 #pragma unroll
-        for (int i = 0; i < 9; ++i) enc_symbol<false>(c, hb, hv[i], s_tab);
+        for (int i = 0; i < 9; ++i) {
+            enc_symbol<false>(c, hb, hv[i], s_tab);
+            flush();
+        }
     }
     // token stream with block forwarding (see the file comment); every step
     // issues the same vector-memory operations: one token load, one block
@@ -512,7 +576,10 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
     auto tok = [&](int i) { return tp[(int64_t)min(i, len - 1) * 64]; };
     // tokens and prefetched blocks live in fixed registers (a ring indexed by
     // the step's phase, 4x unrolled): a register copy of an in-flight load
-    // would make the compiler wait for it at the copy
+    // would make the compiler wait for it at the copy.  (A 4-sample block
+    // prefetch with forwarding from the last 4 samples measured the same
+    // 161-165 ms per 600 frames: the compiler rotates the longer rings
+    // through register copies at the loop latch and waits there.)
     uint32_t tk[4] = {tok(0), tok(1), tok(2), tok(3)};
     int km2 = -1, km1 = -1;
     uint32_t cur[8], prev[8], pre[2][8];
@@ -522,7 +589,7 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
     blk_load(pre[1], st0 + (tk[1] >> 16) * kCtxSize);
     auto step = [&](int i, auto ph_c) {
         constexpr int PH = decltype(ph_c)::value;
-        const uint32_t t0 = tk[PH], t1 = tk[(PH + 1) & 3], t2 = tk[(PH + 2) & 3];
+        const uint32_t t0 = tk[PH], t2 = tk[(PH + 2) & 3];
         const int k0 = (int)(t0 >> 16);
         const int v = (int)(int16_t)(t0 & 0xFFFFu);
         uint32_t b[8];
@@ -535,10 +602,9 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
         // the block of sample i + 2 (used unless sample i or i + 1 forwards it)
         blk_load(pre[PH & 1], st0 + (t2 >> 16) * kCtxSize);
         tk[PH] = tok(i + 4);
-        (void)t1;
         enc_symbol<true>(c, b, v, s_tab);
         blk_store(st0 + k0 * kCtxSize, b);
-        flush();
+        if (PH == 3) flush();
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             prev[j] = cur[j];
@@ -557,8 +623,9 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
     if (i < len) step(i, std::integral_constant<int, 0>{});
     if (i + 1 < len) step(i + 1, std::integral_constant<int, 1>{});
     if (i + 2 < len) step(i + 2, std::integral_constant<int, 2>{});
+    flush();
     // closing 0 bit at state 129 (ffv1enc.c encode_frame), ff_rac_terminate's two flushes
-    (void)enc_rac(c, 129, 0, s_tab);
+    enc_dec(c, 129, false);
     c.range = 0xFF;
     c.low += 0xFF;
     enc_renorm(c);
@@ -803,10 +870,11 @@ extern "C" int64_t pp_ffv1_encode(pp_ffv1_enc *E, const pp_frames *src, int nfra
     const int nwg = (ns + 63) / 64;
     PP_HIP(hipMemsetAsync(E->states, 128, (size_t)kStateBytes * ns, st));  // every context of every slice: 128
     if (a.bytes == 2)
-        hipLaunchKernelGGL(ffv1_model_kernel<uint16_t>, dim3((unsigned)E->rows_max, nwg), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(ffv1_model_kernel<uint16_t>, dim3((unsigned)E->rows_max, nwg), dim3(256), 0, st, a);
     else
-        hipLaunchKernelGGL(ffv1_model_kernel<uint8_t>, dim3((unsigned)E->rows_max, nwg), dim3(64), 0, st, a);
-    hipLaunchKernelGGL(ffv1_code_kernel, dim3(nwg), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(ffv1_model_kernel<uint8_t>, dim3((unsigned)E->rows_max, nwg), dim3(256), 0, st, a);
+    a.lpw = ffv1_lanes_per_wave(64);
+    hipLaunchKernelGGL(ffv1_code_kernel, dim3((ns + a.lpw - 1) / a.lpw), dim3(64), 0, st, a);
     hipLaunchKernelGGL(ffv1_resolve_kernel, dim3(nwg), dim3(64), 0, st, a);
     PP_HIP(hipGetLastError());
     std::vector<int64_t> sizes(ns), off(ns);

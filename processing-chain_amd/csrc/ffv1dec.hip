@@ -85,6 +85,7 @@ struct Ffv1DecArgs {
     int64_t ls[3], fs[3];
     int w, h, bytes, bits, hsub, vsub, nh, nv, nslices, ec;
     int ctx_count;               // contexts per plane set (record's tables)
+    int lpw;                     // slices (active lanes) per 64-lane workgroup: ffv1_lanes_per_wave()
     int64_t state_bytes;         // per slice: 2 * ctx_count * 32 + 64
     uint8_t *states;             // [nslices][state_bytes], primed to 128
     int *status;
@@ -200,7 +201,8 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
         s_q[2][i] = a.quant[512 + i];
     }
     __syncthreads();
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if ((int)threadIdx.x >= a.lpw) return;
+    const int g = blockIdx.x * a.lpw + threadIdx.x;
     if (g >= a.nslices) return;
     const int per = a.nh * a.nv;
     const int frame = g / per, s = g - frame * per;
@@ -465,7 +467,8 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     a.nh = D->nh; a.nv = D->nv; a.nslices = ns; a.ec = D->ec;
     a.ctx_count = D->ctx_count; a.state_bytes = sb;
     a.states = D->states; a.status = D->status; a.tables = D->tables; a.quant = D->dquant;
-    hipLaunchKernelGGL(ffv1_decode_kernel, dim3((ns + 63) / 64), dim3(64), 0, st, a);
+    a.lpw = ffv1_lanes_per_wave(32);
+    hipLaunchKernelGGL(ffv1_decode_kernel, dim3((ns + a.lpw - 1) / a.lpw), dim3(64), 0, st, a);
     PP_HIP(hipGetLastError());
     std::vector<int> status(ns);
     PP_HIP(hipMemcpyAsync(status.data(), D->status, sizeof(int) * ns, hipMemcpyDeviceToHost, st));

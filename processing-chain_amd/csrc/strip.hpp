@@ -94,8 +94,8 @@ __device__ inline void store4(uint8_t *drow, int xo, const int o[4], bool vec, i
 // yuv2packedX with its flat 1 << 18 rounding): every plane stores its 8-bit
 // samples into the one packed row, byte J.pk_off + x * J.pk_step (Y: 1, 2;
 // U: 0, 4; V: 2, 4) -- no planar scratch, no interleave pass.
-// FUSE >= 8 (chain plans, pp_scale_chain_plan_create; register bound for 3 waves per
-// SIMD -- ring2 puts the plan's LDS at ~3 workgroups per CU anyway): 0 = plain plan; 8 / 10 = the
+// FUSE >= 8 (chain plans, pp_scale_chain_plan_create; register budget
+// strip_chain_min_waves): 0 = plain plan; 8 / 10 = the
 // two-stage chain of create_avpvs_segment -- this kernel's 8-bit (OUTB == 8)
 // output is the overlay's yuv420p, and the per-plane mode J.fuse applies
 // libavfilter's auto-inserted yuv420p -> target conversion (FUSE-bit output)
@@ -109,8 +109,17 @@ __device__ inline void store4(uint8_t *drow, int xo, const int o[4], bool vec, i
 // TW = strip width = threads: 256 (4 waves, one per row group) or 512 (8 waves:
 // row group wave >> 1, column half wave & 1; same 4 outputs per lane, half the
 // strips, so half the column-halo staging and 1-KB contiguous row stores)
+// Chain plans (FUSE >= 8): the same per-instance budget rule, with the ring2
+// path's extra registers -- 6 waves where that is spill-free (config 4's
+// <u16, 8, 4, 3, 10>: 79 VGPRs), 4 for windows up to 10 dwords, else 3
+// (tools/check_spills.sh).  Was 3 for every chain instance: 3 workgroups per
+// CU although the plan's LDS (~25 KB) allows 6.
+template <int HW, int VTM>
+constexpr int strip_chain_min_waves() {
+    return (HW <= 5 && VTM <= 3) ? 6 : ((HW <= 10 && VTM <= 5) || (HW == 12 && VTM <= 3)) ? 4 : 3;
+}
 template <typename ST, int OUTB, int HW, int VTM, int FUSE = 0, int TW = 256>
-__global__ __launch_bounds__(TW, (FUSE >= 8 ? 3 : strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
+__global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() : strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
     static_assert(TW == 256 || TW == 512, "strip width");
     extern __shared__ __align__(16) uint16_t lds[];
     const int L = xcd_remap(blockIdx.x, gridDim.x);

@@ -261,6 +261,11 @@ class Ffv1AviWriter:
             d = torch.from_numpy(data[:n * self.fb].reshape(n, self.fb)).to(self.device, non_blocking=False)
         self._put(d, self.put_stream)
 
+    def release(self):
+        """Drop the encoder and the staging batches (device memory) after close()."""
+        self.enc = None
+        self.stages = None
+
     def close(self):
         try:
             if self.fill:
