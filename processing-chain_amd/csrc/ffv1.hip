@@ -169,6 +169,8 @@ struct Ffv1Args {
     int64_t raw_cap;        // dwords per slice
     int32_t *nraw;          // [nslices] records, -1 = overflow
     int lpw;                // slices (active lanes) per 64-lane coder workgroup
+    int debug;              // PIXPATH_FFV1_DEBUG (timing ablation only; the output is wrong):
+                            // 1 no block loads, 2 no block stores, 4 no record flush
 };
 
 __device__ inline int dquant(int d) {  // d already & 0xFF
@@ -600,11 +602,11 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
             blk_sel(b, k0 == km1, cur, tmp);
         }
         // the block of sample i + 2 (used unless sample i or i + 1 forwards it)
-        blk_load(pre[PH & 1], st0 + (t2 >> 16) * kCtxSize);
+        if (!(a.debug & 1)) blk_load(pre[PH & 1], st0 + (t2 >> 16) * kCtxSize);
         tk[PH] = tok(i + 4);
         enc_symbol<true>(c, b, v, s_tab);
-        blk_store(st0 + k0 * kCtxSize, b);
-        if (PH == 3) flush();
+        if (!(a.debug & 2)) blk_store(st0 + k0 * kCtxSize, b);
+        if (PH == 3 && !(a.debug & 4)) flush();
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             prev[j] = cur[j];
@@ -874,6 +876,7 @@ extern "C" int64_t pp_ffv1_encode(pp_ffv1_enc *E, const pp_frames *src, int nfra
     else
         hipLaunchKernelGGL(ffv1_model_kernel<uint8_t>, dim3((unsigned)E->rows_max, nwg), dim3(256), 0, st, a);
     a.lpw = ffv1_lanes_per_wave(64);
+    if (const char *e = std::getenv("PIXPATH_FFV1_DEBUG")) a.debug = std::atoi(e);
     hipLaunchKernelGGL(ffv1_code_kernel, dim3((ns + a.lpw - 1) / a.lpw), dim3(64), 0, st, a);
     hipLaunchKernelGGL(ffv1_resolve_kernel, dim3(nwg), dim3(64), 0, st, a);
     PP_HIP(hipGetLastError());

@@ -116,7 +116,7 @@ __device__ inline void store4(uint8_t *drow, int xo, const int o[4], bool vec, i
 // CU although the plan's LDS (~25 KB) allows 6.
 template <int HW, int VTM>
 constexpr int strip_chain_min_waves() {
-    return (HW <= 5 && VTM <= 3) ? 6 : ((HW <= 10 && VTM <= 5) || (HW == 12 && VTM <= 3)) ? 4 : 3;
+    return (HW <= 4 && VTM <= 3) ? 6 : ((HW <= 10 && VTM <= 5) || (HW == 12 && VTM <= 3)) ? 4 : 3;
 }
 template <typename ST, int OUTB, int HW, int VTM, int FUSE = 0, int TW = 256>
 __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() : strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
@@ -444,29 +444,56 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                 __syncthreads();  // this chunk's first-stage rows are in ring2
                 const int lo2 = chunk2[4 * ci], hi2 = chunk2[4 * ci + 1];
                 const kconst int32_t *vrow2 = as_kconst<int32_t>(J.vrow2);
-                const int vtp2 = J.vtp2;
-                for (int r2 = lo2 + rg; r2 < hi2; r2 += 4) {
-                    const kconst int32_t *row = vrow2 + (int64_t)r2 * 16;
-                    const uint4 *rp = reinterpret_cast<const uint4 *>(ring2 + ((row[0] - base2) >> 1) * TW + cx);
-                    int acc[4];
+                // VT2 tap pairs compile-time; the row records of G2 rows come
+                // through the scalar cache at once (as in the first stage's V
+                // pass: one exposed scalar-load latency per group, not per row)
+                auto pass2 = [&](auto vt_c) {
+                    constexpr int VT2 = decltype(vt_c)::value;
+                    constexpr int G2 = 4;
+                    for (int g0 = lo2 + rg; g0 < hi2; g0 += 4 * G2) {
+                        int vb[G2];
+                        int32_t cf[G2][VT2];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[j] = FUSE == 8 ? 64 << 12 : 1 << (10 + 16 - FUSE);
+                        for (int i = 0; i < G2; ++i) {
+                            const kconst int32_t *row = vrow2 + (int64_t)min(g0 + 4 * i, hi2 - 1) * 16;
+                            vb[i] = row[0];
 #pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        if (jj >= vtp2) break;
-                        const uint4 q = rp[jj * (TW / 4)];
-                        const v2i16 c2 = __builtin_bit_cast(v2i16, row[1 + jj]);
-                        acc[0] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.x), c2, acc[0], false);
-                        acc[1] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.y), c2, acc[1], false);
-                        acc[2] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.z), c2, acc[2], false);
-                        acc[3] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q.w), c2, acc[3], false);
+                            for (int j = 0; j < VT2; ++j) cf[i][j] = row[1 + j];
+                        }
+#pragma unroll
+                        for (int i = 0; i < G2; ++i) {
+                            const int r2 = g0 + 4 * i;
+                            if (r2 >= hi2) break;
+                            const uint4 *rp = reinterpret_cast<const uint4 *>(ring2 + ((vb[i] - base2) >> 1) * TW + cx);
+                            uint4 q[VT2];
+#pragma unroll
+                            for (int j = 0; j < VT2; ++j) q[j] = rp[j * (TW / 4)];
+                            int acc[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) acc[j] = FUSE == 8 ? 64 << 12 : 1 << (10 + 16 - FUSE);
+#pragma unroll
+                            for (int j = 0; j < VT2; ++j) {
+                                const v2i16 c2 = __builtin_bit_cast(v2i16, cf[i][j]);
+                                acc[0] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].x), c2, acc[0], false);
+                                acc[1] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].y), c2, acc[1], false);
+                                acc[2] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].z), c2, acc[2], false);
+                                acc[3] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].w), c2, acc[3], false);
+                            }
+                            if (!lane_any) continue;
+                            constexpr int s2 = FUSE == 8 ? 19 : 11 + 16 - FUSE;
+                            int w[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) w[j] = min(max(acc[j] >> s2, 0), (1 << FUSE) - 1);
+                            store4<FUSE>(dbase + (int64_t)r2 * dls, xo, w, lane_full && a.vec_dst, J.dw);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
                     }
-                    if (!lane_any) continue;
-                    constexpr int s2 = FUSE == 8 ? 19 : 11 + 16 - FUSE;
-                    int w[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) w[j] = min(max(acc[j] >> s2, 0), (1 << FUSE) - 1);
-                    store4<FUSE>(dbase + (int64_t)r2 * dls, xo, w, lane_full && a.vec_dst, J.dw);
+                };
+                switch (J.vtp2) {  // uniform; the host allows <= 4 pairs
+                case 1: pass2(std::integral_constant<int, 1>{}); break;
+                case 2: pass2(std::integral_constant<int, 2>{}); break;
+                case 3: pass2(std::integral_constant<int, 3>{}); break;
+                default: pass2(std::integral_constant<int, 4>{}); break;
                 }
             }
         }

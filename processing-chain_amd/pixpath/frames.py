@@ -13,8 +13,16 @@ from . import formats
 from ._native import pp_frames
 
 
+import os
+
+# layout padding for measurement (bytes added to every row pitch, rows added
+# to every plane of a frame); the kernels take any pitch / frame stride
+_PITCH_PAD = int(os.environ.get("PIXPATH_PITCH_PAD", "0"))
+_ROWS_PAD = int(os.environ.get("PIXPATH_ROWS_PAD", "0"))
+
+
 def _pitch(cols, bps, align=16):
-    b = cols * bps
+    b = cols * bps + _PITCH_PAD
     return ((b + align - 1) // align * align) // bps
 
 
@@ -27,7 +35,8 @@ class FrameBatch:
         dtype = torch.uint16 if bps == 2 else torch.uint8
         if planes is None:
             alloc = torch.zeros if zero else torch.empty
-            planes = [alloc((self.n, r, _pitch(c, bps)), dtype=dtype, device=device) for r, c in self.shapes]
+            planes = [alloc((self.n, r + _ROWS_PAD, _pitch(c, bps)), dtype=dtype, device=device)
+                      for r, c in self.shapes]
         self.planes = planes
         self.bps = bps
 

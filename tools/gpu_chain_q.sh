@@ -1,0 +1,11 @@
+set -o pipefail
+TAG=${1:-cq}
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_chain.py tests/test_gpu_configs.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_$TAG.log; grep -E "^(FAILED|ERROR)" gpurun_out/pytest_$TAG.log | head
+if [ $rc -gt 1 ]; then exit $rc; fi
+for r in 1 2; do
+timeout -k 10 120 python -u bench.py --workload config4 --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/c4_$TAG.json 2>> gpurun_out/c4_$TAG.err || { tail -3 gpurun_out/c4_$TAG.err; exit 1; }
+python3 -c "import json;d=json.load(open('gpurun_out/c4_$TAG.json'));c=d['canvas_chain'];print('c4', c['avg_launch_ms'], c['frac'])"
+done
