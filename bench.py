@@ -367,6 +367,7 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         closers, errs, stats, n = [], [], [], 0
+        pipe_s = []
 
         def close(wr):  # encode + write of PVS k overlap the scale of PVS k + 1
             try:
@@ -374,10 +375,11 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4):
                 stats.append(dict(wr.stats))
             except Exception as e:  # re-raised below
                 errs.append(e)
-            wr.release()
         for k in range(count):
             wr = Ffv1AviWriter(paths[k], dfmt, dw, dh, 60, slices=(8, 8), batch=n_frames, device=dev.index)
+            tp = time.perf_counter()
             n += pl.run(MemReader(), wr)
+            pipe_s.append(round(time.perf_counter() - tp, 3))
             th = threading.Thread(target=close, args=(wr,))
             th.start()
             closers.append(th)
@@ -387,6 +389,7 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4):
         dt = time.perf_counter() - t0
         if errs:
             raise errs[0]
+        stats.append({"pipeline_s": pipe_s})
         return n, dt, stats
 
     try:
@@ -394,13 +397,15 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4):
         n1, dt1, w1 = run(1)
         size = os.path.getsize(paths[0])
         n, dt, ws = run(n_pvs)
+        stages = {"pipeline_s": ws[-1]["pipeline_s"], "encode_and_d2h_s": [round(w["encode_s"], 3) for w in ws[:-1]],
+                  "avi_write_s": [round(w["write_s"], 3) for w in ws[:-1]]}
     finally:
         for p_ in paths:
             if os.path.exists(p_):
                 os.remove(p_)
         os.rmdir(d)
     st = w1[0]
-    return {"frames_per_s": round(n / dt, 1), "frames": n, "pvs": n_pvs, "seconds": round(dt, 3),
+    return {"frames_per_s": round(n / dt, 1), "frames": n, "pvs": n_pvs, "seconds": round(dt, 3), "stages": stages,
             "single_pvs": {"frames_per_s": round(n1 / dt1, 1), "seconds": round(dt1, 3),
                            "breakdown_s": {"ffv1_encode_and_d2h": round(st["encode_s"], 3),
                                            "avi_write": round(st["write_s"], 3)}},

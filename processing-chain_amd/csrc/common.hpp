@@ -59,7 +59,7 @@ inline int ceil_rshift(int a, int s) { return -((-a) >> s); }
 // coder of a slice is one serial chain and a 600-frame batch has only
 // frames x slices chains; fewer lanes per wave trade issue slots for waves.
 // Measured (profiles/r3): the encoder's coder is issue-bound per wave (full
-// waves best), the decoder waits on its context-block loads (32 lanes best).
+// waves best), the decoder waits on its context-block loads (16 lanes best).
 // PIXPATH_FFV1_LPW overrides both (1..64).
 inline int ffv1_lanes_per_wave(int dflt) {
     static const int v = [] {

@@ -467,7 +467,7 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     a.nh = D->nh; a.nv = D->nv; a.nslices = ns; a.ec = D->ec;
     a.ctx_count = D->ctx_count; a.state_bytes = sb;
     a.states = D->states; a.status = D->status; a.tables = D->tables; a.quant = D->dquant;
-    a.lpw = ffv1_lanes_per_wave(32);
+    a.lpw = ffv1_lanes_per_wave(16);
     hipLaunchKernelGGL(ffv1_decode_kernel, dim3((ns + a.lpw - 1) / a.lpw), dim3(64), 0, st, a);
     PP_HIP(hipGetLastError());
     std::vector<int> status(ns);

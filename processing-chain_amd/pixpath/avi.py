@@ -11,6 +11,7 @@ The reader walks the chunks (it needs no index).  Round trips are tested
 here; acceptance by FFmpeg's avidec is unpinned (no FFmpeg in this
 environment).
 """
+import os
 import struct
 from fractions import Fraction
 
@@ -25,7 +26,10 @@ def _chunk(fourcc, payload):
 
 class AviWriter:
     def __init__(self, path, w, h, rate, extradata=b"", fourcc=b"FFV1", riff_limit=RIFF_LIMIT):
-        self.fh = open(path, "wb", buffering=1 << 22)
+        # unbuffered: a packet goes out as one writev of (chunk header, payload,
+        # pad) straight from the caller's buffer -- no copy through a Python
+        # buffer, and the GIL is released for the whole write
+        self.fh = open(path, "wb", buffering=0)
         self.w, self.h, self.rate = int(w), int(h), Fraction(rate)
         self.extradata, self.fourcc, self.limit = bytes(extradata), fourcc, riff_limit
         self.riffs = []       # per RIFF: [riff_start, movi_start, [(data_offset, size, key)]]
@@ -102,12 +106,25 @@ class AviWriter:
                 and self.riffs[-1][2]:
             self._close_movi()
             self._open_movi()
-        off = self.fh.tell() + 8
-        self.fh.write(b"00dc" + struct.pack("<I", n))
-        self.fh.write(data)
-        if n & 1:
-            self.fh.write(b"\0")
-        self.riffs[-1][2].append((off, n, key))
+        pos = self.fh.tell()
+        parts = [b"00dc" + struct.pack("<I", n), data] + ([b"\0"] if n & 1 else [])
+        total, done = 8 + n + (n & 1), 0
+        while done < total:  # writev may write short
+            k = os.writev(self.fh.fileno(), parts)
+            done += k
+            if done < total:
+                self.fh.seek(pos + done)
+                rest, skip = [], done
+                for b in parts:
+                    b = memoryview(b).cast("B")
+                    if skip >= len(b):
+                        skip -= len(b)
+                        continue
+                    rest.append(b[skip:])
+                    skip = 0
+                parts = rest
+        self.fh.seek(pos + total)
+        self.riffs[-1][2].append((pos + 8, n, key))
         self.total += 1
         self.max_size = max(self.max_size, n)
 

@@ -88,6 +88,31 @@ class Ffv1Encoder:
         return out
 
 
+_POOL_LOCK = threading.Lock()
+_POOL = {}  # (fmt, w, h, slices, max_frames, device) -> [idle Ffv1Encoder]
+
+
+def acquire_encoder(fmt, w, h, slices=(8, 8), max_frames=600, device=None):
+    """An idle encoder of this geometry from the process's pool, else a new
+    one.  An encoder holds ~20 GB of HBM for a 600-frame 1080p batch (tokens,
+    records, slice buffers, context states); consecutive PVSes of one process
+    reuse it instead of allocating and freeing it per PVS."""
+    key = (formats.fmt(fmt).id, int(w), int(h), tuple(int(v) for v in slices), int(max_frames),
+           context(device).device)
+    with _POOL_LOCK:
+        idle = _POOL.get(key)
+        if idle:
+            return idle.pop()
+    return Ffv1Encoder(fmt, w, h, slices=slices, max_frames=max_frames, device=device)
+
+
+def release_encoder(enc):
+    """Return an encoder from acquire_encoder() to the pool."""
+    key = (enc.fmt.id, enc.w, enc.h, enc.slices, enc.max_frames, enc.ctx.device)
+    with _POOL_LOCK:
+        _POOL.setdefault(key, []).append(enc)
+
+
 class Ffv1Decoder:
     """FFV1 v3 intra decoder on the GPU (one lane per slice): the AVPVS read
     back for the CPVS stage.  ``decode(packets, sizes)`` takes the frame
@@ -151,7 +176,7 @@ class Ffv1AviWriter:
         self.w, self.h = int(w), int(h)
         self.fb = formats.frame_bytes(self.fmt, w, h)
         self.batch = int(batch)
-        self.enc = Ffv1Encoder(self.fmt, w, h, slices=slices, max_frames=self.batch, device=device)
+        self.enc = acquire_encoder(self.fmt, w, h, slices=slices, max_frames=self.batch, device=device)
         self.device = torch.device("cuda", self.enc.ctx.device)
         self.stages = [FrameBatch.interleaved(self.fmt, w, h, self.batch, device=self.device) for _ in range(2)]
         self.free = [threading.Event(), threading.Event()]
@@ -262,7 +287,9 @@ class Ffv1AviWriter:
         self._put(d, self.put_stream)
 
     def release(self):
-        """Drop the encoder and the staging batches (device memory) after close()."""
+        """After close(): the encoder goes back to the pool, the staging batches are dropped."""
+        if self.enc is not None:
+            release_encoder(self.enc)
         self.enc = None
         self.stages = None
 
@@ -278,6 +305,7 @@ class Ffv1AviWriter:
             self._check()
         finally:
             self.avi.close()
+            self.release()
 
 
 class Ffv1AviReader:
