@@ -86,6 +86,8 @@ struct Ffv1DecArgs {
     int w, h, bytes, bits, hsub, vsub, nh, nv, nslices, ec;
     int ctx_count;               // contexts per plane set (record's tables)
     int lpw;                     // slices (active lanes) per 64-lane workgroup: ffv1_lanes_per_wave()
+    int debug;                   // PIXPATH_FFV1_DEBUG (timing ablation only; the output is wrong):
+                                 // 8 no state-block loads, 16 no state-block stores
     int64_t state_bytes;         // per slice: 2 * ctx_count * 32 + 64
     uint8_t *states;             // [nslices][state_bytes], primed to 128
     int *status;
@@ -275,8 +277,8 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
                 if (neg) ctx = -ctx;
                 const int key = key0 + ctx;
                 if (key != cur_key) {
-                    if (cur_key >= 0) dblk_store(st0 + cur_key * kCtx, blk);
-                    dblk_load(blk, st0 + key * kCtx);
+                    if (cur_key >= 0 && !(a.debug & 16)) dblk_store(st0 + cur_key * kCtx, blk);
+                    if (!(a.debug & 8)) dblk_load(blk, st0 + key * kCtx);
                     cur_key = key;
                 }
                 int diff = dec_symbol<true>(d, blk, s_tab, bad);
@@ -468,6 +470,7 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     a.ctx_count = D->ctx_count; a.state_bytes = sb;
     a.states = D->states; a.status = D->status; a.tables = D->tables; a.quant = D->dquant;
     a.lpw = ffv1_lanes_per_wave(16);
+    if (const char *e = std::getenv("PIXPATH_FFV1_DEBUG")) a.debug = std::atoi(e);
     hipLaunchKernelGGL(ffv1_decode_kernel, dim3((ns + a.lpw - 1) / a.lpw), dim3(64), 0, st, a);
     PP_HIP(hipGetLastError());
     std::vector<int> status(ns);
