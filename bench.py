@@ -82,6 +82,7 @@ def parse():
     ap.add_argument("--cpu-sweep", default="16,64", help="extra thread counts timed (shorter) beside the full width")
     ap.add_argument("--no-siti-file", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--overlap", action="store_true", help="SI/TI on a second stream, concurrent with the scaler")
     return ap.parse_args()
 
 
@@ -470,6 +471,7 @@ def main():
     torch.cuda.synchronize()
 
     ev = []
+    side = torch.cuda.Stream(dev) if args.overlap else None
 
     def step(timed):
         res = []
@@ -481,11 +483,24 @@ def main():
             scaler(src, outs[i % len(outs)])
             if timed:
                 b.record()
+            if luma is not None and side is not None:
+                # --overlap: SI/TI of the SRC on its own stream, concurrent with the
+                # scaler (independent inputs): the VALU-bound Sobel under the
+                # store-bound scaler.  Events then time each kernel under co-execution.
+                with torch.cuda.stream(side):
+                    if timed:
+                        b2 = torch.cuda.Event(enable_timing=True)
+                        b2.record(side)
+                    res.append(ops.siti(luma, 10, stream=side))
+                    if timed:
+                        c.record(side)
+                        ev.append((a, b, b2, c))
+                continue
             if luma is not None:
                 res.append(ops.siti(luma, 10))
             if timed:
                 c.record()
-                ev.append((a, b, c))
+                ev.append((a, b, b, c))
         gathered = None
         if siti_wh:
             si = torch.stack([r[0] for r in res]).cpu().numpy() if res else None
@@ -508,8 +523,8 @@ def main():
     batch.barrier(world)
     elapsed = batch.max_over_ranks(time.perf_counter() - t0, world)
 
-    scale_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(1, len(ev))
-    siti_ms = sum(b.elapsed_time(c) for _, b, c in ev) / max(1, len(ev)) if siti_wh else None
+    scale_ms = sum(a.elapsed_time(b) for a, b, _, _ in ev) / max(1, len(ev))
+    siti_ms = sum(b2.elapsed_time(c) for _, _, b2, c in ev) / max(1, len(ev)) if siti_wh else None
     frames_total = total * n * args.steps
     value = frames_total / elapsed
     per_rank = batch.gather_values(len(mine), rank, world)
