@@ -645,9 +645,19 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
 
 // ---- 3. bytes: renorm_encoder's outstanding-byte machine ----------------------
 __global__ __launch_bounds__(64) void ffv1_resolve_kernel(const Ffv1Args a) {
-    __shared__ uint32_t s_crc[256];
-    for (int i = threadIdx.x; i < 256; i += 64) s_crc[i] = reinterpret_cast<const uint32_t *>(a.tables + 512)[i];
+    // slice-by-4 CRC tables: s_crc[k][i] = the byte table advanced by k zero
+    // bytes, so a whole output word updates the CRC with 4 independent lookups
+    // (one LDS latency on the chain per 4 bytes instead of per byte)
+    __shared__ uint32_t s_crc[4][256];
+    for (int i = threadIdx.x; i < 256; i += 64) s_crc[0][i] = reinterpret_cast<const uint32_t *>(a.tables + 512)[i];
     __syncthreads();
+    for (int k = 1; k < 4; ++k) {
+        for (int i = threadIdx.x; i < 256; i += 64) {
+            const uint32_t p = s_crc[k - 1][i];
+            s_crc[k][i] = (p << 8) ^ s_crc[0][p >> 24];
+        }
+        __syncthreads();
+    }
     if ((int)threadIdx.x >= a.rlpw) return;
     const int g = blockIdx.x * a.rlpw + threadIdx.x;
     if (g >= a.nslices) return;
@@ -664,9 +674,10 @@ __global__ __launch_bounds__(64) void ffv1_resolve_kernel(const Ffv1Args a) {
     bool over = false;
     auto emit = [&](uint32_t v) {
         v &= 0xFFu;
-        crc = (crc << 8) ^ s_crc[(crc >> 24) ^ v];
         word |= v << ((nb & 3) * 8);
-        if ((nb & 3) == 3) {
+        if ((nb & 3) == 3) {  // bytes b0..b3 = word's bytes 0..3, b0 first
+            crc = s_crc[3][(crc >> 24) ^ (word & 0xFFu)] ^ s_crc[2][((crc >> 16) & 0xFFu) ^ ((word >> 8) & 0xFFu)] ^
+                  s_crc[1][((crc >> 8) & 0xFFu) ^ ((word >> 16) & 0xFFu)] ^ s_crc[0][(crc & 0xFFu) ^ (word >> 24)];
             if ((nb >> 2) < capw) dst[nb >> 2] = word;
             else over = true;
             word = 0;
@@ -674,10 +685,7 @@ __global__ __launch_bounds__(64) void ffv1_resolve_kernel(const Ffv1Args a) {
         ++nb;
     };
     int ob = -1, oc = 0;
-    uint32_t pair = 0;
-    for (int j = 0; j < nraw; ++j) {
-        if (!(j & 1)) pair = raw[j >> 1];
-        const uint32_t r = (j & 1) ? pair >> 16 : pair & 0xFFFFu;
+    auto record = [&](uint32_t r) {
         const int hi = (int)(r & 0x1FFu);
         const bool exact = (r >> 9) & 1u;
         if (ob < 0) {
@@ -693,8 +701,31 @@ __global__ __launch_bounds__(64) void ffv1_resolve_kernel(const Ffv1Args a) {
         } else {
             ++oc;
         }
+    };
+    // records 8 at a time (16 B), the blocks two ahead in flight: a record
+    // load per pair of records used to put the memory latency on the chain
+    const uint4 *rp = reinterpret_cast<const uint4 *>(raw);  // 16-B aligned (raw_cap % 4 == 0)
+    const int nblk = (nraw + 7) >> 3;
+    auto blk = [&](int b) { return rp[min(b, nblk - 1)]; };  // past the end: rereads the last block
+    uint4 q[2] = {nblk > 0 ? blk(0) : make_uint4(0, 0, 0, 0), nblk > 1 ? blk(1) : make_uint4(0, 0, 0, 0)};
+    auto block = [&](int b, uint4 &slot) {
+        const uint4 v = slot;
+        slot = blk(b + 2);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        const int m = min(8, nraw - 8 * b);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k >= m) break;
+            record((k & 1) ? w[k >> 1] >> 16 : w[k >> 1] & 0xFFFFu);
+        }
+    };
+    for (int b = 0; b < nblk; b += 2) {
+        block(b, q[0]);
+        if (b + 1 < nblk) block(b + 1, q[1]);
     }
     if (nb & 3) {
+        for (int64_t i = 0; i < (nb & 3); ++i)  // the last partial word, byte by byte
+            crc = (crc << 8) ^ s_crc[0][(crc >> 24) ^ ((word >> (8 * i)) & 0xFFu)];
         if ((nb >> 2) < capw) dst[nb >> 2] = word;
         else over = true;
     }
