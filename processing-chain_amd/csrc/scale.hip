@@ -726,7 +726,12 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
         if (hp[c].h.taps != ht && P->f[c].compact(src_w, ht, &hp[c].h, &err))
             PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
         pair_rows(hp[c]);
-        if (plan_tiles(hp[c], src_w, src_h, dst_w, dst_h, &P->lds_bytes, &err, c && one_seg_chroma ? 1 << 20 : 0, cho_max))
+        // chain plans (one_seg_chroma): the chroma ring of the fused second stage
+        // needs the short chunks; PIXPATH_CHAIN_LUMA_CHO (measurement) sets luma's
+        int cho_c = cho_max;
+        if (!c && one_seg_chroma)
+            if (const char *e = std::getenv("PIXPATH_CHAIN_LUMA_CHO")) cho_c = std::max(1, atoi(e));
+        if (plan_tiles(hp[c], src_w, src_h, dst_w, dst_h, &P->lds_bytes, &err, c && one_seg_chroma ? 1 << 20 : 0, cho_c))
             PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
     }
     // strip_kernel eligibility: the generic tiling fits 256-column strips,
