@@ -529,7 +529,11 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
     if (g >= a.nslices) return;
     const SliceGeo q = slice_geo(g, a.w, a.h, a.nh, a.nv, a.hsub, a.vsub);
     const int len = q.len();
-    uint8_t *const st0 = a.states + (int64_t)g * kStateBytes;
+    // context states of the 64-slice group interleaved by slice: context k of
+    // slice g at [g / 64][k][g % 64] -- a 128-B line holds one context of 4
+    // slices (a context that is hot in one slice is hot in its neighbours)
+    uint8_t *const st0 = a.states + (int64_t)(g >> 6) * (64 * kStateBytes) + (g & 63) * kCtxSize;
+    constexpr int kCtxStride = 64 * kCtxSize;
     // tokens of slice g: group g / 64 of the modelling layout, lane g % 64
     const uint32_t *tp = a.tok + (int64_t)(g >> 6) * a.tok_len * 64 + (g & 63);
     Enc c;
@@ -587,8 +591,8 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
     uint32_t cur[8], prev[8], pre[2][8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) cur[i] = prev[i] = 0u;
-    blk_load(pre[0], st0 + (tk[0] >> 16) * kCtxSize);
-    blk_load(pre[1], st0 + (tk[1] >> 16) * kCtxSize);
+    blk_load(pre[0], st0 + (tk[0] >> 16) * kCtxStride);
+    blk_load(pre[1], st0 + (tk[1] >> 16) * kCtxStride);
     auto step = [&](int i, auto ph_c) {
         constexpr int PH = decltype(ph_c)::value;
         const uint32_t t0 = tk[PH], t2 = tk[(PH + 2) & 3];
@@ -602,10 +606,10 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
             blk_sel(b, k0 == km1, cur, tmp);
         }
         // the block of sample i + 2 (used unless sample i or i + 1 forwards it)
-        if (!(a.debug & 1)) blk_load(pre[PH & 1], st0 + (t2 >> 16) * kCtxSize);
+        if (!(a.debug & 1)) blk_load(pre[PH & 1], st0 + (t2 >> 16) * kCtxStride);
         tk[PH] = tok(i + 4);
         enc_symbol<true>(c, b, v, s_tab);
-        if (!(a.debug & 2)) blk_store(st0 + k0 * kCtxSize, b);
+        if (!(a.debug & 2)) blk_store(st0 + k0 * kCtxStride, b);
         if (PH == 3 && !(a.debug & 4)) flush();
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -848,7 +852,7 @@ extern "C" int pp_ffv1_encoder_create(pp_ctx *ctx, int fmt, int w, int h, int sl
     E->raw_cap = E->cap / 2 + 4;  // two renorm records (one per output byte) per dword
     PP_HIP(hipSetDevice(ctx->device));
     PP_HIP(hipMalloc(&E->slices, E->cap * ns));
-    PP_HIP(hipMalloc(&E->states, (size_t)kStateBytes * ns));
+    PP_HIP(hipMalloc(&E->states, (size_t)kStateBytes * ns64));
     PP_HIP(hipMalloc(&E->sizes, sizeof(int64_t) * ns));
     PP_HIP(hipMalloc(&E->off, sizeof(int64_t) * ns));
     PP_HIP(hipMalloc(&E->crcs, sizeof(uint32_t) * ns));
@@ -902,7 +906,7 @@ extern "C" int64_t pp_ffv1_encode(pp_ffv1_enc *E, const pp_frames *src, int nfra
     a.tables = E->tables;
     a.tok = E->tok; a.tok_len = E->tok_len; a.raw = E->raw; a.raw_cap = E->raw_cap; a.nraw = E->nraw;
     const int nwg = (ns + 63) / 64;
-    PP_HIP(hipMemsetAsync(E->states, 128, (size_t)kStateBytes * ns, st));  // every context of every slice: 128
+    PP_HIP(hipMemsetAsync(E->states, 128, (size_t)kStateBytes * ((ns + 63) / 64 * 64), st));  // every context of every slice: 128
     if (a.bytes == 2)
         hipLaunchKernelGGL(ffv1_model_kernel<uint16_t>, dim3((unsigned)E->rows_max, nwg), dim3(256), 0, st, a);
     else
