@@ -88,6 +88,15 @@ class Ffv1Encoder:
         return out
 
 
+def default_slices():
+    """The AVPVS writers' slice grid: PIXPATH_FFV1_SLICES ("HxV"), else 8x8."""
+    import os
+    v = os.environ.get("PIXPATH_FFV1_SLICES", "8x8").lower().split("x")
+    if len(v) != 2 or not all(t.isdigit() and int(t) > 0 for t in v):
+        raise ValueError("PIXPATH_FFV1_SLICES must be HxV, e.g. 16x16")
+    return int(v[0]), int(v[1])
+
+
 _POOL_LOCK = threading.Lock()
 _POOL = {}  # (fmt, w, h, slices, max_frames, device) -> [idle Ffv1Encoder]
 
@@ -169,9 +178,13 @@ class Ffv1AviWriter:
     worker thread on its own stream while the next batch fills (two staging
     batches), its packets come back in one pinned D2H and go into the AVI."""
 
-    def __init__(self, path, fmt, w, h, rate, slices=(8, 8), batch=600, device=None):
+    def __init__(self, path, fmt, w, h, rate, slices=None, batch=600, device=None):
+        """slices: the FFV1 slice grid (default PIXPATH_FFV1_SLICES, else 8x8;
+        16x16 encodes ~1.3x faster at ~7 % larger files)."""
         from . import avi
         from .frames import FrameBatch
+        if slices is None:
+            slices = default_slices()
         self.fmt = formats.fmt(fmt)
         self.w, self.h = int(w), int(h)
         self.fb = formats.frame_bytes(self.fmt, w, h)

@@ -192,3 +192,16 @@ def test_interleaved_batch_on_a_storage_slice():
         v = FrameBatch.interleaved("yuv422p10le", 16, 6, 4 - k, device="cpu", storage=b.storage[k:])
         for p in range(3):
             assert torch.equal(v.view(p)[0], b.view(p)[k])
+
+
+def test_ffv1_writer_slice_grid_setting(monkeypatch):
+    """PIXPATH_FFV1_SLICES picks the AVPVS writers' FFV1 slice grid (default 8x8)."""
+    from pixpath import ffv1
+    monkeypatch.delenv("PIXPATH_FFV1_SLICES", raising=False)
+    assert ffv1.default_slices() == (8, 8)
+    monkeypatch.setenv("PIXPATH_FFV1_SLICES", "16x16")
+    assert ffv1.default_slices() == (16, 16)
+    for bad in ("16", "0x4", "ax4"):
+        monkeypatch.setenv("PIXPATH_FFV1_SLICES", bad)
+        with pytest.raises(ValueError):
+            ffv1.default_slices()
