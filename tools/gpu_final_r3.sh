@@ -18,7 +18,7 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/p
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_$TAG -o run -- python3 bench.py --steps 2 --warmup 0 --pvs-total 2 --pool 2 --no-cpu-baseline --no-pipeline --no-siti-file --no-e2e > gpurun_out/prof_write_$TAG.log 2>&1 || { tail -5 gpurun_out/prof_write_$TAG.log; exit 1; }
 python3 tools/pmc_traffic.py gpurun_out/prof_fetch_$TAG/run_counter_collection.csv gpurun_out/prof_write_$TAG/run_counter_collection.csv gpurun_out/prof_kt_$TAG/run_kernel_trace.csv gpurun_out/pmc_traffic_$TAG.json 600 > /dev/null || exit 1
 grep -E "pp::" gpurun_out/prof_kt_$TAG/run_kernel_stats.csv | cut -d, -f1-4 | cut -c1-140
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt_ffv1_$TAG -o run -- python3 bench.py --workload ffv1 --steps 2 --warmup 1 > gpurun_out/bench_ffv1_$TAG.json 2> gpurun_out/bench_ffv1_$TAG.err || { tail -5 gpurun_out/bench_ffv1_$TAG.err; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt_ffv1_$TAG -o run -- python3 bench.py --workload ffv1 --ffv1-concurrent 1 --steps 2 --warmup 1 > gpurun_out/bench_ffv1_$TAG.json 2> gpurun_out/bench_ffv1_$TAG.err || { tail -5 gpurun_out/bench_ffv1_$TAG.err; exit 1; }
 grep -E "ffv1" gpurun_out/kt_ffv1_$TAG/run_kernel_stats.csv | cut -d, -f1-4
 for wl in config3-10 config3-8 config4; do
   timeout -k 10 200 python -u bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline --no-pipeline > gpurun_out/bench_${wl}_$TAG.json 2>> gpurun_out/bench_$TAG.err || { tail -3 gpurun_out/bench_$TAG.err; exit 1; }
