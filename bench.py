@@ -275,7 +275,7 @@ def siti_file(dev, n=600, w=1920, h=1080):
                     "H2D (copy stream) -> siti_kernel (compute stream) -> per-frame SI/TI on the host"}
 
 
-def pcie_pipeline(wl, n_frames, dev):
+def pcie_pipeline(wl, n_frames, dev, batch=60):
     """Pinned host frames -> H2D -> scaler -> D2H through pixpath.pipeline
     (two streams, double buffers); PCIe-inclusive, reported beside `value`."""
     import numpy as np
@@ -302,7 +302,7 @@ def pcie_pipeline(wl, n_frames, dev):
             pass
     sc = ops.Scaler(sfmt, sw, sh, dfmt, dw, dh, flags=flags, device=dev.index)
     stage = Stage(sfmt, sw, sh, dfmt, dw, dh, lambda s, d, st: sc(s, d, stream=st))
-    pl = Pipeline(stage, batch=60, device=dev.index)
+    pl = Pipeline(stage, batch=batch, device=dev.index)
     pl.run(MemReader(), NullWriter())  # warm-up pass (pinned buffers, plan)
     import torch
     torch.cuda.synchronize()
@@ -310,7 +310,7 @@ def pcie_pipeline(wl, n_frames, dev):
     n = pl.run(MemReader(), NullWriter())
     dt = time.perf_counter() - t0
     return {"frames_per_s": round(n / dt, 1), "pcie_gbs": round(n * (in_fb + out_fb) / dt / 1e9, 2),
-            "frames": n, "batch": 60,
+            "frames": n, "batch": batch,
             "note": "host pinned -> H2D (copy stream) -> strip_kernel (compute stream) -> D2H -> host; "
                     "host fill of the pinned input is included, decode/encode are not"}
 
