@@ -324,3 +324,36 @@ def test_writer_device_batches_and_canvas_repeat(gpu, tmp_path):
         for p in range(3):
             np.testing.assert_array_equal(dec[p], want[p])
     assert pk[50] == pk[59] == pk[49]
+
+
+def test_writer_pool_reuses_encoder_across_pvses(gpu, tmp_path):
+    """Two AVPVS writers in a row in one process (the reference's runner
+    feeding several PVSes): the second takes the first's encoder from the
+    pool, and both AVIs decode to their own frames (context states and slice
+    buffers start clean for every batch)."""
+    import torch
+    from pixpath import avi, ffv1
+    from pixpath.frames import FrameBatch
+    rng = np.random.default_rng(77)
+    w, h = 320, 180
+    encs = []
+    for k in range(2):
+        frames = [synth.noise_frame(rng, po.YUV422P10LE, w, h) for _ in range(5)] if k == 0 else \
+            [synth.smooth_frame(3 + i, po.YUV422P10LE, w, h) for i in range(7)]
+        path = str(tmp_path / ("PVS%d.avi" % k))
+        wr = ffv1.Ffv1AviWriter(path, "yuv422p10le", w, h, 60, slices=(4, 4), batch=8, device=gpu)
+        encs.append(wr.enc)
+        src = FrameBatch.interleaved("yuv422p10le", w, h, len(frames), device=gpu)
+        for i, f in enumerate(frames):
+            for p in range(3):
+                src.view(p)[i].copy_(torch.from_numpy(f[p].astype(np.uint16)))
+        wr.write_device(src)
+        wr.close()
+        info, pk = avi.read_packets(path)
+        assert len(pk) == len(frames)
+        for i, f in enumerate(frames):
+            rc, dec = ref.decode_frame(info["extradata"], pk[i], w, h, 10, 1, 0)
+            assert rc == 0
+            for p in range(3):
+                np.testing.assert_array_equal(dec[p], f[p], err_msg="PVS %d frame %d plane %d" % (k, i, p))
+    assert encs[1] is encs[0]
