@@ -339,14 +339,20 @@ __global__ __launch_bounds__(256) void ffv1_model_kernel(const Ffv1Args a) {
     int *const my = s_row + lane * kMLane;
     for (int x0 = 0; x0 < pw_max; x0 += kMX) {
         if (x0) __syncthreads();  // the previous chunk's LDS reads are done
-        // stage columns x0 - 1 .. x0 + 64 of the row above and the row of every lane
-        for (int e = t; e < 64 * 2 * kMS; e += 256) {
-            const int j = e / (2 * kMS), rem = e - j * (2 * kMS);
-            const int rw = rem >= kMS ? 1 : 0, col = rem - rw * kMS, x = x0 - 1 + col;
-            int v = 0;
-            if (x >= 0 && x < s_info[j][0] && (rw || s_info[j][1]))
-                v = reinterpret_cast<const ST *>(s_ptr[j][rw])[x];
-            s_row[j * kMLane + rw * kMS + col] = v;
+        // stage columns x0 - 1 .. x0 + 64 of the row above and the row of every
+        // lane: thread t takes half t & 1 of segment t >> 1 (lane j, row rw),
+        // so its row pointer and bounds are fixed for the chunk (no per-sample
+        // divisions or LDS lookups); successive samples of a thread hit L1
+        {
+            const int seg = t >> 1, j = seg >> 1, rw = seg & 1, c0 = (t & 1) * (kMS / 2);
+            const ST *rp = reinterpret_cast<const ST *>(s_ptr[j][rw]);
+            const int lim = (rw || s_info[j][1]) ? s_info[j][0] : 0;  // row above absent: zeros
+            int *dst = s_row + j * kMLane + rw * kMS;
+#pragma unroll 11
+            for (int col = c0; col < c0 + kMS / 2; ++col) {
+                const int x = x0 - 1 + col;
+                dst[col] = (x >= 0 && x < lim) ? (int)rp[x] : 0;
+            }
         }
         __syncthreads();
         const int xe = min(pw, x0 + kMX);
