@@ -1170,6 +1170,7 @@ int launch_chain(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, i
     a.dither = P->si.depth > 8;
     a.vec_src = 1;
     a.vec_dst = 1;
+    if (const char *e = std::getenv("PIXPATH_SCALE_DEBUG")) a.debug = atoi(e);
     for (int p = 0; p < 3; ++p)
         a.vec_dst &= aligned(a.dst[p], a.dls[p], nframes > 1 ? a.dfs[p] : 0, P->chain_out == 8 ? 4 : 8);
     const int vtm = strip_vtm_bucket(std::max(P->fjob[0].vtp, P->fjob[1].vtp));

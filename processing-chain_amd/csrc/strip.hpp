@@ -440,7 +440,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
         }
         if constexpr (FUSE >= 8) {
             // ---- second stage (fuse 2): vertical filter of the ring2 rows ----
-            if (J.fuse == 2) {
+            if (J.fuse == 2 && !(a.debug & 16)) {  // debug 16: no second stage (timing only)
                 __syncthreads();  // this chunk's first-stage rows are in ring2
                 const int lo2 = chunk2[4 * ci], hi2 = chunk2[4 * ci + 1];
                 const kconst int32_t *vrow2 = as_kconst<int32_t>(J.vrow2);
