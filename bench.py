@@ -64,6 +64,35 @@ def frame_bytes(fmt, w, h):
     return formats.frame_bytes(fmt, w, h)
 
 
+# Settings a product run may carry (device choice, backend, codec); every
+# other PIXPATH_* variable is a measurement override (tools/) and voids a
+# bench line: bench.py refuses to run with one unless --allow-tuning, and then
+# records them in the line.  The product library reads no environment at all
+# (csrc/common.hpp PP_KNOB); these guard the Python side and PIXPATH_LIB.
+PRODUCT_ENV = {"PIXPATH_DEVICE", "PIXPATH_SLOT_DIR", "PIXPATH_BACKEND", "PIXPATH_FFV1", "PIXPATH_FFV1_SLICES",
+               "PIXPATH_SPINNER", "PIXPATH_HOME"}
+
+
+def tuning_overrides():
+    """PIXPATH_* variables of this process that are not product settings."""
+    from pixpath import _native
+    bad = {k: v for k, v in os.environ.items() if k.startswith("PIXPATH_") and k not in PRODUCT_ENV}
+    default_lib = os.path.join(ROOT, "processing-chain_amd", "pixpath", "libpixpath.so")
+    if "PIXPATH_LIB" in bad and os.path.realpath(bad["PIXPATH_LIB"]) == os.path.realpath(default_lib):
+        del bad["PIXPATH_LIB"]
+    if os.path.realpath(_native.LIB_PATH) != os.path.realpath(default_lib):
+        bad.setdefault("PIXPATH_LIB", _native.LIB_PATH)
+    return bad
+
+
+def library_id():
+    """sha256[:16] of the loaded libpixpath.so (what the line measured)."""
+    import hashlib
+    from pixpath import _native
+    with open(_native.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -84,6 +113,10 @@ def parse():
     ap.add_argument("--no-siti-file", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--overlap", action="store_true", help="SI/TI on a second stream, concurrent with the scaler")
+    ap.add_argument("--allow-tuning", action="store_true",
+                    help="run with PIXPATH_* measurement overrides set (tools/ only; recorded in the line)")
+    ap.add_argument("--e2e-pvs", type=int, default=4, help="PVSes in a row for the e2e_avpvs line")
+    ap.add_argument("--cpu-e2e-seconds", type=float, default=4.0, help="CPU counterpart of e2e_avpvs: sample length")
     return ap.parse_args()
 
 
@@ -188,7 +221,7 @@ def cpu_baseline(args, wl):
            "scale_fps": top["scale_fps"], "sweep": sweep,
            "per_thread_scale_fps": round(top["scale_fps"] / top["threads"], 2)}
     if args.workload == "config2":
-        out["e2e"] = cpu_e2e(top["threads"], wl, sws, outs, po)
+        out["e2e"] = cpu_e2e(top["threads"], wl, sws, outs, po, seconds=args.cpu_e2e_seconds)
     if siti_wh:
         out["siti_fps"] = top["siti_fps"]
         out["sample"] = ("%d-thread oracle C restatement (oracle/pixoracle.c + siti_oracle.c, gcc -O3), the best point "
@@ -205,11 +238,12 @@ def cpu_baseline(args, wl):
     return out
 
 
-def cpu_e2e(nt, wl, sws, outs, po, frames_per_thread=2):
+def cpu_e2e(nt, wl, sws, outs, po, seconds=4.0):
     """CPU counterpart of e2e_avpvs: per frame, the oracle's scaler then the
     oracle's FFV1 encoder (oracle/ffv1_oracle.c, the same bitstream as the GPU
     encoder, 8x8 slices) on the compressible content e2e_avpvs uses, on nt
-    threads; decode and file writes excluded (a lower bound on the CPU time)."""
+    threads for `seconds` (every thread finishes the frame it started);
+    decode and file writes excluded (a lower bound on the CPU time)."""
     import threading
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -226,7 +260,7 @@ def cpu_e2e(nt, wl, sws, outs, po, frames_per_thread=2):
     done = [0] * nt
 
     def work(t):
-        for _ in range(frames_per_thread):
+        while time.perf_counter() - t0 < seconds:
             sws[t].scale_into(planes, outs[t], 1)
             ffv1_ref.encode_frame(outs[t], depth, hs, vs, 8, 8)
             done[t] += 1
@@ -238,8 +272,8 @@ def cpu_e2e(nt, wl, sws, outs, po, frames_per_thread=2):
         x.join()
     dt = time.perf_counter() - t0
     return {"frames_per_s": round(sum(done) / dt, 2), "threads": nt, "frames": sum(done), "seconds": round(dt, 2),
-            "sample": "%d frames: oracle scale 720p->1080p yuv422p10le %s + oracle FFV1 encode (8x8 slices) per "
-                      "frame, %d threads" % (sum(done), flags, nt)}
+            "sample": "%d frames in %.1f s: oracle scale 720p->1080p yuv422p10le %s + oracle FFV1 encode (8x8 "
+                      "slices) per frame, %d threads" % (sum(done), dt, flags, nt)}
 
 
 def siti_file(dev, n=600, w=1920, h=1080):
@@ -315,7 +349,7 @@ def pcie_pipeline(wl, n_frames, dev, batch=60):
                     "host fill of the pinned input is included, decode/encode are not"}
 
 
-def e2e_avpvs(wl, n_frames, dev, n_pvs=4):
+def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None):
     """The product path of `cli avpvs --gpu-ffv1` end to end (SURVEY.md 8d's
     third row): dense host frames -> pinned batches -> H2D -> strip_kernel ->
     FFV1 encode of the DEVICE output (no D2H of pixels) -> packets D2H -> AVI
@@ -326,13 +360,15 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4):
     feeds them (lib/cmd_utils.py:93-101): each writer encodes and writes its
     PVS on its own worker thread and stream while the next PVS is scaled, so
     the scale, encode and file-write stages of consecutive PVSes overlap.
-    `single_pvs` is the same path for one PVS with nothing to overlap.  Never
-    `value`."""
+    The encoder pool holds `depth` encoders (with their staging batch) before
+    the timed region, as a long-running writer process keeps them; writer
+    construction is timed as its own stage (`setup_s`).  `single_pvs` is the
+    same path for one PVS with nothing to overlap.  Never `value`."""
     import tempfile
     import threading
     import numpy as np
     import torch
-    from pixpath import formats, ops
+    from pixpath import ffv1, formats, ops
     from pixpath.ffv1 import Ffv1AviWriter
     from pixpath.pipeline import Pipeline, Stage
     sfmt, sw, sh, dfmt, dw, dh, flags, _ = wl
@@ -364,12 +400,17 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4):
     pl = Pipeline(stage, batch=60, device=dev.index)
     d = tempfile.mkdtemp(prefix="pixpath_e2e_")
     paths = [os.path.join(d, "PVS%d.avi" % k) for k in range(n_pvs)]
+    depth = depth or n_pvs  # every PVS of the run can be in flight at once
+    t_res = time.perf_counter()
+    made = ffv1.reserve_encoders(dfmt, dw, dh, depth, slices=(8, 8), max_frames=n_frames, device=dev.index)
+    torch.cuda.synchronize()
+    reserve_s = time.perf_counter() - t_res
 
     def run(count):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         closers, errs, stats, n = [], [], [], 0
-        pipe_s = []
+        setup_s, pipe_s = [], []
 
         def close(wr):  # encode + write of PVS k overlap the scale of PVS k + 1
             try:
@@ -378,45 +419,68 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4):
             except Exception as e:  # re-raised below
                 errs.append(e)
         for k in range(count):
+            tw = time.perf_counter()
             wr = Ffv1AviWriter(paths[k], dfmt, dw, dh, 60, slices=(8, 8), batch=n_frames, device=dev.index)
             tp = time.perf_counter()
             n += pl.run(MemReader(), wr)
-            pipe_s.append(round(time.perf_counter() - tp, 3))
+            te = time.perf_counter()
+            setup_s.append(round(tp - tw, 4))
+            pipe_s.append(round(te - tp, 4))
             th = threading.Thread(target=close, args=(wr,))
             th.start()
             closers.append(th)
             del wr
+        t_main = time.perf_counter()
         for th in closers:
             th.join()
-        dt = time.perf_counter() - t0
+        t_end = time.perf_counter()
         if errs:
             raise errs[0]
-        stats.append({"pipeline_s": pipe_s})
-        return n, dt, stats
+        dt = t_end - t0
+        order = sorted(stats, key=lambda w: w["timeline"][0][0] if w["timeline"] else 0)
+        st = {"setup_s": setup_s, "pipeline_s": pipe_s, "tail_s": round(t_end - t_main, 4),
+              # per PVS, seconds from the run's start: batch queued, frames ready on the
+              # GPU (encode starts), packets on the host, packets written, AVI closed
+              "timeline": [[round(x - t0, 4) for x in (w["timeline"][0][0], w["timeline"][0][2],
+                                                       w["timeline"][0][3], w["timeline"][0][4], w["closed_at"])]
+                           for w in order if w["timeline"]],
+              "encode_and_d2h_s": [round(w["encode_s"], 4) for w in order],
+              "avi_write_s": [round(w["write_s"], 4) for w in order],
+              "encode_launches": [w["launches"] for w in order]}
+        # the main thread's stages plus the wait for the last writers: the wall time
+        st["explained_s"] = round(sum(setup_s) + sum(pipe_s) + st["tail_s"], 4)
+        st["explained_frac"] = round(st["explained_s"] / dt, 4)
+        return n, dt, st
 
     try:
-        run(1)  # warm-up (allocations, kernel loads)
+        run(1)  # warm-up (kernel loads, pinned buffers, the pipeline's device batches)
         n1, dt1, w1 = run(1)
         size = os.path.getsize(paths[0])
         n, dt, ws = run(n_pvs)
-        stages = {"pipeline_s": ws[-1]["pipeline_s"], "encode_and_d2h_s": [round(w["encode_s"], 3) for w in ws[:-1]],
-                  "avi_write_s": [round(w["write_s"], 3) for w in ws[:-1]]}
     finally:
         for p_ in paths:
-            if os.path.exists(p_):
-                os.remove(p_)
+            for q_ in (p_, p_ + ".part"):
+                if os.path.exists(q_):
+                    os.remove(q_)
         os.rmdir(d)
-    st = w1[0]
-    return {"frames_per_s": round(n / dt, 1), "frames": n, "pvs": n_pvs, "seconds": round(dt, 3), "stages": stages,
-            "single_pvs": {"frames_per_s": round(n1 / dt1, 1), "seconds": round(dt1, 3),
-                           "breakdown_s": {"ffv1_encode_and_d2h": round(st["encode_s"], 3),
-                                           "avi_write": round(st["write_s"], 3)}},
+    enc_mem = None
+    try:
+        e = ffv1.acquire_encoder(dfmt, dw, dh, slices=(8, 8), max_frames=n_frames, device=dev.index)
+        enc_mem = e.memory_bytes + sum(b.storage.numel() for b in (e.stages or []))
+        ffv1.release_encoder(e)
+    except Exception:
+        pass
+    ffv1.clear_pool()
+    return {"frames_per_s": round(n / dt, 1), "frames": n, "pvs": n_pvs, "seconds": round(dt, 3), "stages": ws,
+            "single_pvs": {"frames_per_s": round(n1 / dt1, 1), "seconds": round(dt1, 3), "stages": w1},
+            "encoder_pool": {"depth": depth, "created": made, "reserve_s": round(reserve_s, 3),
+                             "bytes_per_writer": enc_mem},
             "avi_bytes_per_pvs": size, "compression": round(n1 * frame_bytes(dfmt, dw, dh) / size, 3),
             "note": "%d PVSes of %d frames: host frames -> pinned batches of 60 -> H2D -> strip_kernel "
                     "(720p->1080p yuv422p10le lanczos) -> FFV1 v3 encode on the device output (8x8 slices, one "
                     "batch per PVS, the writer's worker thread and stream) -> packets D2H -> AVI file; consecutive "
-                    "PVSes overlap; decode of the SRC bitstream excluded (ffmpeg is absent on the box)"
-                    % (n_pvs, n_frames)}
+                    "PVSes overlap; %d pooled encoders reserved before timing; decode of the SRC bitstream "
+                    "excluded (ffmpeg is absent on the box)" % (n_pvs, n_frames, depth)}
 
 
 def make_inputs(wl, n, seed, dev):
@@ -442,6 +506,11 @@ def make_inputs(wl, n, seed, dev):
 def main():
     args = parse()
     from pixpath import batch
+    over = tuning_overrides()
+    if over and not args.allow_tuning:
+        print("bench: refusing to run with measurement overrides set: %s (they change kernel plans or outputs; "
+              "unset them, or pass --allow-tuning for a tools/ run)" % " ".join(sorted(over)), file=sys.stderr)
+        return 2
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # parent: start one rank per GPU and relay their exit status (no HIP here)
         sys.exit(batch.spawn_local(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
@@ -573,8 +642,11 @@ def main():
             "traffic": traffic,
             "algorithmic_bytes_per_launch": bytes_pf * n,
             "avg_launch_ms": round(scale_ms, 4),
+            "plan": dict(scaler.stats, kernel_path=scaler.kernel_path),
         },
         "cpu_baseline": None,
+        "library": library_id(),
+        "tuning_overrides": tuning_overrides() or None,
     }
     if siti_wh:
         luma_b = siti_wh[0] * siti_wh[1] * 2
@@ -591,7 +663,7 @@ def main():
     if world == 1 and siti_wh and not args.no_siti_file:
         out["siti_file"] = siti_file(dev)
     if world == 1 and args.workload == "config2" and not args.no_e2e:
-        out["e2e_avpvs"] = e2e_avpvs(wl, 600, dev)
+        out["e2e_avpvs"] = e2e_avpvs(wl, 600, dev, n_pvs=args.e2e_pvs)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, wl)
         ce = out["cpu_baseline"].get("e2e") if out["cpu_baseline"] else None
@@ -664,7 +736,8 @@ def bench_stall(args, rank, world, dev):
                                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                                        "traffic": None, "algorithmic_bytes_per_launch": 2 * fb * n,
                                        "avg_launch_ms": round(ms, 4)},
-                          "canvas_chain": canvas, "cpu_baseline": None}), flush=True)
+                          "canvas_chain": canvas, "cpu_baseline": None, "library": library_id(),
+                          "tuning_overrides": tuning_overrides() or None}), flush=True)
     return 0
 
 
@@ -767,7 +840,7 @@ def bench_ffv1(args, rank, world, dev):
            "decode": {"frames_per_s": round(world * n / ddt, 1), "ms_per_step": round(ddt * 1e3, 3),
                       "lossless": lossless, "note": "packets from host memory (H2D included)"},
            "concurrent": conc,
-           "roofline": None}
+           "roofline": None, "library": library_id(), "tuning_overrides": tuning_overrides() or None}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import ffv1_ref

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PP_ABI_VERSION 4
+#define PP_ABI_VERSION 5
 
 /* return codes */
 #define PP_OK 0
@@ -51,6 +51,9 @@ enum pp_pix_fmt {
 #define PP_SWS_BICUBIC 0x4
 #define PP_SWS_LANCZOS 0x200
 #define PP_SWS_PARAM_DEFAULT 123456.0
+/* ABI v5: plan flag selecting the general scale_kernel even where the strip
+ * kernel applies (both are bit-exact; tests run every plan through both). */
+#define PP_PLAN_GENERIC 0x10000000
 
 /*
  * A batch of `nframes` frames.  Plane p of frame f starts at
@@ -262,6 +265,18 @@ int pp_ffv1_encoder_destroy(pp_ffv1_enc *enc);
 int pp_ffv1_extradata(const pp_ffv1_enc *enc, uint8_t *out, int cap);
 int64_t pp_ffv1_encode(pp_ffv1_enc *enc, const pp_frames *src, int nframes, uint8_t *dst,
                        int64_t dst_cap, int64_t *frame_sizes, void *stream);
+/* ABI v5.  pp_ffv1_encode_packets: the same encode into the encoder's own
+ * device packet buffer (grown as needed, kept across calls); *packets points
+ * at the packets back to back, valid until the next encode; returns the total
+ * bytes.  The encoder sizes its per-slice renorm records for content coding at
+ * 2:1 or better and re-codes a batch in halves when a slice needs more, so
+ * the packets never depend on that sizing (pp_ffv1_encode_stats: launches of
+ * the last encode, 1 unless it was split).  pp_ffv1_encoder_memory: device
+ * bytes the encoder holds. */
+int64_t pp_ffv1_encode_packets(pp_ffv1_enc *enc, const pp_frames *src, int nframes, int64_t *frame_sizes,
+                               const uint8_t **packets, void *stream);
+int pp_ffv1_encode_stats(const pp_ffv1_enc *enc, int *launches);
+int pp_ffv1_encoder_memory(const pp_ffv1_enc *enc, int64_t *bytes);
 /* FFV1 decoder (the CPVS stage reads the AVPVS back, lib/ffmpeg.py:1149):
  * version 3 intra streams with the range coder's default state table, one
  * quantisation table set of up to 3 inputs, <= 256 slices, 8/10-bit

@@ -13,6 +13,19 @@
 
 #include "../../include/pixpath.h"
 
+// Measurement knobs (ablation bits, tuning overrides) exist only in the
+// ablation build (`make ablate`, tools/ scripts): there PP_KNOB reads the
+// environment and PP_ABLATE(x) passes a kernel's ablation bits through.  The
+// product library is built without PIXPATH_ABLATE: it never reads the
+// environment, and every ablation branch folds to its product path.
+#ifdef PIXPATH_ABLATE
+#define PP_KNOB(name) std::getenv(name)
+#define PP_ABLATE(bits) (bits)
+#else
+#define PP_KNOB(name) ((const char *)nullptr)
+#define PP_ABLATE(bits) 0
+#endif
+
 namespace pp {
 
 void set_error(const char *fmt, ...);
@@ -60,10 +73,10 @@ inline int ceil_rshift(int a, int s) { return -((-a) >> s); }
 // frames x slices chains; fewer lanes per wave trade issue slots for waves.
 // Measured (profiles/r3): the encoder's coder is issue-bound per wave (full
 // waves best), the decoder waits on its context-block loads (16 lanes best).
-// PIXPATH_FFV1_LPW overrides both (1..64).
+// PIXPATH_FFV1_LPW overrides both (1..64; ablation build only).
 inline int ffv1_lanes_per_wave(int dflt) {
     static const int v = [] {
-        const char *e = std::getenv("PIXPATH_FFV1_LPW");
+        const char *e = PP_KNOB("PIXPATH_FFV1_LPW");
         const int x = e ? std::atoi(e) : 0;
         return x >= 1 && x <= 64 ? x : 0;
     }();

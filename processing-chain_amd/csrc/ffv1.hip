@@ -41,132 +41,28 @@
 
 #include "common.hpp"
 #include "device.hpp"
+#include "ffv1host.hpp"
 
 namespace pp {
 
-constexpr int kFfv1Ctx = 666;   // (11^3 + 1) / 2 contexts per plane set
-constexpr int kCtxSize = 32;    // state bytes per context
+constexpr int kCtxSize = kFfv1CtxBytes;  // state bytes per context
 constexpr int kStateBytes = 2 * kFfv1Ctx * kCtxSize;  // luma and chroma context sets of one slice
-
-// ---- host range coder (configuration record) and state tables -------------
-struct HostRC {
-    int low = 0, range = 0xFF00, oc = 0, ob = -1;
-    uint8_t zero[256], one[256];
-    std::vector<uint8_t> out;
-    void byte(int v) { out.push_back((uint8_t)v); }
-    void renorm() {
-        while (range < 0x100) {
-            if (ob < 0) {
-                ob = low >> 8;
-            } else if (low <= 0xFF00) {
-                byte(ob);
-                for (; oc; oc--) byte(0xFF);
-                ob = low >> 8;
-            } else if (low >= 0x10000) {
-                byte(ob + 1);
-                for (; oc; oc--) byte(0x00);
-                ob = (low >> 8) - 0x100;
-            } else {
-                oc++;
-            }
-            low = (low & 0xFF) << 8;
-            range <<= 8;
-        }
-    }
-    void rac(uint8_t *st, int bit) {
-        const int r1 = (range * *st) >> 8;
-        if (!bit) {
-            range -= r1;
-            *st = zero[*st];
-        } else {
-            low += range - r1;
-            range = r1;
-            *st = one[*st];
-        }
-        renorm();
-    }
-    void symbol(uint8_t *st, int v) {  // unsigned
-        if (!v) {
-            rac(st, 1);
-            return;
-        }
-        int e = 0;
-        while ((v >> (e + 1)) > 0) ++e;
-        rac(st, 0);
-        for (int i = 0; i < e; i++) rac(st + 1 + std::min(i, 9), 1);
-        rac(st + 1 + std::min(e, 9), 0);
-        for (int i = e - 1; i >= 0; i--) rac(st + 22 + std::min(i, 9), (v >> i) & 1);
-    }
-    size_t terminate() {
-        range = 0xFF;
-        low += 0xFF;
-        renorm();
-        range = 0xFF;
-        renorm();
-        return out.size();
-    }
-};
-
-// ff_build_rac_states(c, 0.05 * 2^32, 256 - 8): the default state-transition table
-void rac_states(uint8_t zero[256], uint8_t one[256]) {
-    const int64_t kOne = (int64_t)1 << 32;
-    const int64_t factor = (int64_t)(0.05 * (double)((int64_t)1 << 32));
-    const int max_p = 256 - 8;
-    std::memset(zero, 0, 256);
-    std::memset(one, 0, 256);
-    int64_t p = kOne / 2;
-    int last_p8 = 0;
-    for (int i = 0; i < 128; i++) {
-        int p8 = (int)((256 * p + kOne / 2) >> 32);
-        if (p8 <= last_p8) p8 = last_p8 + 1;
-        if (last_p8 && last_p8 < 256 && p8 <= max_p) one[last_p8] = (uint8_t)p8;
-        p += ((kOne - p) * factor + kOne / 2) >> 32;
-        last_p8 = p8;
-    }
-    for (int i = 256 - max_p; i <= max_p; i++) {
-        if (one[i]) continue;
-        p = (i * kOne + 128) >> 8;
-        p += ((kOne - p) * factor + kOne / 2) >> 32;
-        int p8 = (int)((256 * p + kOne / 2) >> 32);
-        if (p8 <= i) p8 = i + 1;
-        if (p8 > max_p) p8 = max_p;
-        one[i] = (uint8_t)p8;
-    }
-    for (int i = 1; i < 255; i++) zero[i] = (uint8_t)(256 - one[256 - i]);
-}
-
-// AV_CRC_32_IEEE: polynomial 0x04C11DB7, MSB first, initial 0, no final xor
-void crc_table(uint32_t t[256]) {
-    for (uint32_t i = 0; i < 256; i++) {
-        uint32_t c = i << 24;
-        for (int j = 0; j < 8; j++) c = (c << 1) ^ ((c & 0x80000000u) ? 0x04C11DB7u : 0u);
-        t[i] = c;
-    }
-}
-
-// quantiser of the context inputs on (d & 0xFF): min(5, bit length of |d|), odd-mirrored
-inline int quant_host(int i) {
-    if (i >= 128) return -quant_host(i == 128 ? 127 : 256 - i);
-    int q = 0;
-    while (i) { q++; i >>= 1; }
-    return std::min(q, 5);
-}
 
 // ---- device ---------------------------------------------------------------
 struct Ffv1Args {
     const uint8_t *src[3];
     int64_t ls[3], fs[3];
     int w, h, bytes, bits, hsub, vsub, nh, nv, nslices;  // nslices = frames * nh * nv
-    uint8_t *out;           // [nslices][cap] slice bytes (ffv1_resolve_kernel)
-    int64_t cap;
+    int64_t cap;            // per-slice output bytes (the 24-bit footer field bounds it)
     uint8_t *states;        // [nslices][kStateBytes], primed to 128
     int64_t *sizes;         // [nslices] coded bytes, -1 = overflow
     uint32_t *crcs;         // [nslices] CRC-32 of the coded bytes
     const uint8_t *tables;  // zero[256], one[256], crc table (1 KB)
     uint32_t *tok;          // [nslices / 64][tok_len][64] tokens
     int64_t tok_len;        // tokens per slice, max over the grid
-    uint32_t *raw;          // [nslices][raw_cap] renorm records, two per dword
-    int64_t raw_cap;        // dwords per slice
+    uint32_t *raw;          // [nslices][raw_cap] renorm records, two per dword; ffv1_resolve_kernel
+                            // overwrites them in place with the slice bytes (bytes trail records)
+    int64_t raw_cap;        // dwords per slice (this launch: the budget over its slices)
     int32_t *nraw;          // [nslices] records, -1 = overflow
     int lpw;                // slices (active lanes) per 64-lane coder workgroup
     int rlpw;               // the same for ffv1_resolve_kernel
@@ -612,11 +508,11 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
             blk_sel(b, k0 == km1, cur, tmp);
         }
         // the block of sample i + 2 (used unless sample i or i + 1 forwards it)
-        if (!(a.debug & 1)) blk_load(pre[PH & 1], st0 + (t2 >> 16) * kCtxStride);
+        if (!(PP_ABLATE(a.debug) & 1)) blk_load(pre[PH & 1], st0 + (t2 >> 16) * kCtxStride);
         tk[PH] = tok(i + 4);
         enc_symbol<true>(c, b, v, s_tab);
-        if (!(a.debug & 2)) blk_store(st0 + k0 * kCtxStride, b);
-        if (PH == 3 && !(a.debug & 4)) flush();
+        if (!(PP_ABLATE(a.debug) & 2)) blk_store(st0 + k0 * kCtxStride, b);
+        if (PH == 3 && !(PP_ABLATE(a.debug) & 4)) flush();
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             prev[j] = cur[j];
@@ -676,9 +572,13 @@ __global__ __launch_bounds__(64) void ffv1_resolve_kernel(const Ffv1Args a) {
         a.sizes[g] = -1;
         return;
     }
+    // the slice bytes go over the slice's own records: byte k is emitted only
+    // after record k + 1 (record r sits at bytes 2r, 2r + 1), and the blocks
+    // in flight are ahead of both, so a word is written only where the records
+    // have already been read
     const uint32_t *raw = a.raw + (int64_t)g * a.raw_cap;
-    uint32_t *dst = reinterpret_cast<uint32_t *>(a.out + (int64_t)g * a.cap);
-    const int64_t capw = a.cap >> 2;
+    uint32_t *dst = a.raw + (int64_t)g * a.raw_cap;
+    const int64_t capw = a.raw_cap;
     int64_t nb = 0;  // bytes emitted
     uint32_t word = 0, crc = 0;
     bool over = false;
@@ -739,7 +639,7 @@ __global__ __launch_bounds__(64) void ffv1_resolve_kernel(const Ffv1Args a) {
         if ((nb >> 2) < capw) dst[nb >> 2] = word;
         else over = true;
     }
-    a.sizes[g] = over || nb + 8 > a.cap ? -1 : nb;
+    a.sizes[g] = over || nb + 8 > a.cap || nb > capw * 4 ? -1 : nb;
     a.crcs[g] = crc;
 }
 
@@ -772,14 +672,29 @@ struct pp_ffv1_enc {
     pp_ctx *ctx = nullptr;
     int fmt = 0, w = 0, h = 0, nh = 1, nv = 1, max_frames = 0;
     FmtInfo fi{};
-    int64_t cap = 0;           // per-slice output bytes
-    int64_t tok_len = 0, raw_cap = 0, rows_max = 0;
-    uint8_t *slices = nullptr, *states = nullptr, *tables = nullptr;
+    int64_t cap = 0;           // per-slice output bytes (worst case, < 2^24)
+    int64_t full_raw = 0;      // record dwords per slice for that worst case
+    int64_t budget = 0;        // record dwords of the whole `raw` allocation
+    int64_t tok_len = 0, rows_max = 0;
+    uint8_t *states = nullptr, *tables = nullptr;
     int64_t *sizes = nullptr, *off = nullptr;
     uint32_t *crcs = nullptr, *tok = nullptr, *raw = nullptr;
     int32_t *nraw = nullptr;
+    uint8_t *pk = nullptr;     // frame packets of the last encode, back to back
+    int64_t pk_cap = 0, pk_len = 0;
+    int launches = 0;          // launches of the last encode (> 1: a batch was split)
     std::vector<uint8_t> extradata;
 };
+
+// Record budget.  A slice's records (one 16-bit record per output byte) are
+// sized per LAUNCH: the encoder holds `budget` dwords for all of them, and a
+// launch of m frames gives each slice budget / (slices * m).  The default
+// budget holds a full batch at half the raw sample bytes per slice (FFV1 codes
+// video content at 2-4:1); a launch in which some slice runs out is re-coded
+// as two launches of half the frames (twice the records per slice), down to
+// the worst case (uniform noise: ~1.1x the raw bytes), so the output never
+// depends on the budget.  Tokens stay sized for the whole batch.
+constexpr int kBudgetDiv = 3;  // budget per slice = worst case / 3 (~0.5x the raw sample bytes)
 
 extern "C" int pp_ffv1_encoder_create(pp_ctx *ctx, int fmt, int w, int h, int slices_h, int slices_v,
                                       int max_frames, pp_ffv1_enc **out) {
@@ -794,45 +709,8 @@ extern "C" int pp_ffv1_encoder_create(pp_ctx *ctx, int fmt, int w, int h, int sl
     std::unique_ptr<pp_ffv1_enc> E(new pp_ffv1_enc());
     E->ctx = ctx; E->fmt = fmt; E->w = w; E->h = h; E->nh = slices_h; E->nv = slices_v; E->fi = fi;
     E->max_frames = max_frames;
-    // configuration record (RFC 9043 4.2, ffv1enc.c write_extradata)
-    {
-        HostRC c;
-        rac_states(c.zero, c.one);
-        uint8_t st[kCtxSize];
-        std::memset(st, 128, sizeof(st));
-        const int v1[] = {3, 4, 1, 0, fi.depth};  // version, micro_version, coder_type, colorspace, bits
-        for (int v : v1) c.symbol(st, v);
-        c.rac(st, 1);  // chroma_planes
-        c.symbol(st, fi.hsub);
-        c.symbol(st, fi.vsub);
-        c.rac(st, 0);  // extra_plane
-        c.symbol(st, slices_h - 1);
-        c.symbol(st, slices_v - 1);
-        c.symbol(st, 1);  // quant_table_set_count
-        for (int t = 0; t < 5; t++) {
-            uint8_t qs[kCtxSize];
-            std::memset(qs, 128, sizeof(qs));
-            int last = 0, i;
-            for (i = 1; i < 128; i++)
-                if (t < 3 && quant_host(i) != quant_host(i - 1)) {
-                    c.symbol(qs, i - last - 1);
-                    last = i;
-                }
-            c.symbol(qs, i - last - 1);
-        }
-        c.rac(st, 0);       // states_coded
-        c.symbol(st, 1);    // ec
-        c.symbol(st, 1);    // intra
-        uint8_t s129 = 129;
-        c.rac(&s129, 0);
-        c.terminate();
-        uint32_t t[256];
-        crc_table(t);
-        uint32_t crc = 0;
-        for (uint8_t b : c.out) crc = (crc << 8) ^ t[(crc >> 24) ^ b];
-        E->extradata = c.out;
-        for (int k = 3; k >= 0; k--) E->extradata.push_back((uint8_t)(crc >> (8 * k)));
-    }
+    // configuration record (RFC 9043 4.2, ffv1enc.c write_extradata; ffv1host.cpp)
+    E->extradata = ffv1_write_record(fi.depth, fi.hsub, fi.vsub, slices_h, slices_v);
     if (!ctx) {  // host-only: configuration record only
         *out = E.release();
         return PP_OK;
@@ -855,15 +733,16 @@ extern "C" int pp_ffv1_encoder_create(pp_ctx *ctx, int fmt, int w, int h, int sl
     // than the 24-bit footer size field (FFmpeg asserts < 1 << 24) is refused
     E->cap = ((raw * 3 / 2 + 4096) + 255) & ~int64_t(255);
     E->cap = std::min<int64_t>(E->cap, ((int64_t)1 << 24) - 256);
-    E->raw_cap = E->cap / 2 + 4;  // two renorm records (one per output byte) per dword
+    E->full_raw = (E->cap / 2 + 4 + 3) & ~int64_t(3);  // two records (one per output byte) per dword, 16-B rows
+    // every slice of one frame at the worst case always fits (the last split)
+    E->budget = std::max<int64_t>(ns * (E->full_raw / kBudgetDiv), (int64_t)per * E->full_raw);
     PP_HIP(hipSetDevice(ctx->device));
-    PP_HIP(hipMalloc(&E->slices, E->cap * ns));
     PP_HIP(hipMalloc(&E->states, (size_t)kStateBytes * ns64));
     PP_HIP(hipMalloc(&E->sizes, sizeof(int64_t) * ns));
     PP_HIP(hipMalloc(&E->off, sizeof(int64_t) * ns));
     PP_HIP(hipMalloc(&E->crcs, sizeof(uint32_t) * ns));
     PP_HIP(hipMalloc(&E->tok, sizeof(uint32_t) * (size_t)(ns64 * len_max)));
-    PP_HIP(hipMalloc(&E->raw, sizeof(uint32_t) * (size_t)(ns * E->raw_cap)));
+    PP_HIP(hipMalloc(&E->raw, sizeof(uint32_t) * (size_t)E->budget));
     PP_HIP(hipMalloc(&E->nraw, sizeof(int32_t) * ns));
     PP_HIP(hipMalloc(&E->tables, 512 + 1024));
     uint8_t tab[512 + 1024];
@@ -876,8 +755,8 @@ extern "C" int pp_ffv1_encoder_create(pp_ctx *ctx, int fmt, int w, int h, int sl
 
 extern "C" int pp_ffv1_encoder_destroy(pp_ffv1_enc *E) {
     if (!E) return PP_OK;
-    for (void *p : {(void *)E->slices, (void *)E->states, (void *)E->sizes, (void *)E->off, (void *)E->crcs,
-                    (void *)E->tables, (void *)E->tok, (void *)E->raw, (void *)E->nraw})
+    for (void *p : {(void *)E->states, (void *)E->sizes, (void *)E->off, (void *)E->crcs, (void *)E->tables,
+                    (void *)E->tok, (void *)E->raw, (void *)E->nraw, (void *)E->pk})
         if (p) (void)hipFree(p);
     delete E;
     return PP_OK;
@@ -890,65 +769,139 @@ extern "C" int pp_ffv1_extradata(const pp_ffv1_enc *E, uint8_t *out, int cap) {
     return n;
 }
 
-extern "C" int64_t pp_ffv1_encode(pp_ffv1_enc *E, const pp_frames *src, int nframes, uint8_t *dst, int64_t dst_cap,
-                                  int64_t *frame_sizes, void *stream) {
-    if (!E || !src || !dst || !frame_sizes || nframes < 0) PP_FAIL(PP_ERR_INVALID, "null argument");
+extern "C" int pp_ffv1_encoder_memory(const pp_ffv1_enc *E, int64_t *bytes) {
+    if (!E || !bytes) PP_FAIL(PP_ERR_INVALID, "null argument");
+    const int64_t ns = (int64_t)E->nh * E->nv * E->max_frames, ns64 = (ns + 63) / 64 * 64;
+    *bytes = E->ctx ? (int64_t)kStateBytes * ns64 + (8 + 8 + 4 + 4) * ns + 4 * ns64 * E->tok_len + 4 * E->budget +
+                          1536 + E->pk_cap
+                    : 0;
+    return PP_OK;
+}
+
+// Grow the packet buffer to `need` bytes keeping its first `keep` bytes.
+static int pk_reserve(pp_ffv1_enc *E, int64_t need, int64_t keep, hipStream_t st) {
+    if (need <= E->pk_cap) return PP_OK;
+    const int64_t cap = std::max<int64_t>(need, E->pk_cap + E->pk_cap / 2);
+    uint8_t *p = nullptr;
+    PP_HIP(hipMalloc(&p, cap));
+    if (keep) {
+        if (hipMemcpyAsync(p, E->pk, keep, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) {
+            (void)hipFree(p);
+            PP_FAIL(PP_ERR_HIP, "packet buffer copy failed");
+        }
+    }
+    if (E->pk) PP_HIP(hipFree(E->pk));
+    E->pk = p;
+    E->pk_cap = cap;
+    return PP_OK;
+}
+
+extern "C" int64_t pp_ffv1_encode_packets(pp_ffv1_enc *E, const pp_frames *src, int nframes, int64_t *frame_sizes,
+                                          const uint8_t **packets, void *stream) {
+    if (!E || !src || !frame_sizes || nframes < 0) PP_FAIL(PP_ERR_INVALID, "null argument");
     if (!E->ctx) PP_FAIL(PP_ERR_INVALID, "host-only encoder cannot encode");
     if (nframes > E->max_frames) PP_FAIL(PP_ERR_INVALID, "%d frames > max_frames %d", nframes, E->max_frames);
+    if (packets) *packets = nullptr;
+    E->pk_len = 0;
+    E->launches = 0;
     if (nframes == 0) return 0;
     hipStream_t st = static_cast<hipStream_t>(stream);
     PP_HIP(hipSetDevice(E->ctx->device));
     const int per = E->nh * E->nv;
-    const int ns = per * nframes;
-    Ffv1Args a{};
-    for (int p = 0; p < 3; ++p) {
-        a.src[p] = static_cast<const uint8_t *>(src->data[p]);
-        a.ls[p] = src->linesize[p];
-        a.fs[p] = src->frame_stride[p];
-    }
-    a.w = E->w; a.h = E->h; a.bytes = E->fi.depth > 8 ? 2 : 1; a.bits = E->fi.depth;
-    a.hsub = E->fi.hsub; a.vsub = E->fi.vsub; a.nh = E->nh; a.nv = E->nv; a.nslices = ns;
-    a.out = E->slices; a.cap = E->cap; a.states = E->states; a.sizes = E->sizes; a.crcs = E->crcs;
-    a.tables = E->tables;
-    a.tok = E->tok; a.tok_len = E->tok_len; a.raw = E->raw; a.raw_cap = E->raw_cap; a.nraw = E->nraw;
-    const int nwg = (ns + 63) / 64;
-    PP_HIP(hipMemsetAsync(E->states, 128, (size_t)kStateBytes * ((ns + 63) / 64 * 64), st));  // every context of every slice: 128
-    if (a.bytes == 2)
-        hipLaunchKernelGGL(ffv1_model_kernel<uint16_t>, dim3((unsigned)E->rows_max, nwg), dim3(256), 0, st, a);
-    else
-        hipLaunchKernelGGL(ffv1_model_kernel<uint8_t>, dim3((unsigned)E->rows_max, nwg), dim3(256), 0, st, a);
-    a.lpw = ffv1_lanes_per_wave(64);
-    if (const char *e = std::getenv("PIXPATH_FFV1_DEBUG")) a.debug = std::atoi(e);
-    hipLaunchKernelGGL(ffv1_code_kernel, dim3((ns + a.lpw - 1) / a.lpw), dim3(64), 0, st, a);
-    // the byte machine is one dependent chain per slice over its records; full
-    // waves measured best (64 / 16 / 8 lanes: 16.3 / 18.1 / 25.2 ms per 600 frames)
-    a.rlpw = 64;
-    if (const char *e = std::getenv("PIXPATH_FFV1_RLPW")) a.rlpw = std::max(1, std::min(64, std::atoi(e)));
-    hipLaunchKernelGGL(ffv1_resolve_kernel, dim3((ns + a.rlpw - 1) / a.rlpw), dim3(64), 0, st, a);
-    PP_HIP(hipGetLastError());
-    std::vector<int64_t> sizes(ns), off(ns);
-    PP_HIP(hipMemcpyAsync(sizes.data(), E->sizes, sizeof(int64_t) * ns, hipMemcpyDeviceToHost, st));
-    PP_HIP(hipStreamSynchronize(st));
     int64_t total = 0;
-    for (int f = 0; f < nframes; ++f) {
-        int64_t fsz = 0;
-        for (int s = 0; s < per; ++s) {
-            const int64_t n = sizes[f * per + s];
-            if (n < 0) PP_FAIL(PP_ERR_NOMEM, "frame %d slice %d exceeds its %lld-byte buffer", f, s, (long long)E->cap);
-            if (n + 8 >= ((int64_t)1 << 24))  // the footer's 24-bit size field (ffv1enc.c asserts the same)
-                PP_FAIL(PP_ERR_UNSUPPORTED, "frame %d slice %d: %lld bytes exceed the 24-bit slice size", f, s,
-                        (long long)n);
-            off[f * per + s] = total + fsz;
-            fsz += n + 8;
+    int f0 = 0, m = nframes;
+    std::vector<int64_t> sizes, off;
+    while (f0 < nframes) {
+        m = std::min(m, nframes - f0);
+        const int ns = per * m;
+        // records per slice for this launch: the budget over its slices, at most the worst case
+        const int64_t rcap = std::min<int64_t>(E->full_raw, E->budget / ns / 4 * 4);
+        Ffv1Args a{};
+        for (int p = 0; p < 3; ++p) {
+            a.src[p] = static_cast<const uint8_t *>(src->data[p]) + (int64_t)f0 * src->frame_stride[p];
+            a.ls[p] = src->linesize[p];
+            a.fs[p] = src->frame_stride[p];
         }
-        frame_sizes[f] = fsz;
-        total += fsz;
+        a.w = E->w; a.h = E->h; a.bytes = E->fi.depth > 8 ? 2 : 1; a.bits = E->fi.depth;
+        a.hsub = E->fi.hsub; a.vsub = E->fi.vsub; a.nh = E->nh; a.nv = E->nv; a.nslices = ns;
+        a.cap = E->cap; a.states = E->states; a.sizes = E->sizes; a.crcs = E->crcs;
+        a.tables = E->tables;
+        a.tok = E->tok; a.tok_len = E->tok_len; a.raw = E->raw; a.raw_cap = rcap; a.nraw = E->nraw;
+        const int nwg = (ns + 63) / 64;
+        PP_HIP(hipMemsetAsync(E->states, 128, (size_t)kStateBytes * nwg * 64, st));  // every context of every slice: 128
+        if (a.bytes == 2)
+            hipLaunchKernelGGL(ffv1_model_kernel<uint16_t>, dim3((unsigned)E->rows_max, nwg), dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL(ffv1_model_kernel<uint8_t>, dim3((unsigned)E->rows_max, nwg), dim3(256), 0, st, a);
+        a.lpw = ffv1_lanes_per_wave(64);
+        if (const char *e = PP_KNOB("PIXPATH_FFV1_DEBUG")) a.debug = std::atoi(e);
+        hipLaunchKernelGGL(ffv1_code_kernel, dim3((ns + a.lpw - 1) / a.lpw), dim3(64), 0, st, a);
+        // the byte machine is one dependent chain per slice over its records; full
+        // waves measured best (64 / 16 / 8 lanes: 16.3 / 18.1 / 25.2 ms per 600 frames)
+        a.rlpw = 64;
+        if (const char *e = PP_KNOB("PIXPATH_FFV1_RLPW")) a.rlpw = std::max(1, std::min(64, std::atoi(e)));
+        hipLaunchKernelGGL(ffv1_resolve_kernel, dim3((ns + a.rlpw - 1) / a.rlpw), dim3(64), 0, st, a);
+        PP_HIP(hipGetLastError());
+        ++E->launches;
+        sizes.resize(ns);
+        off.resize(ns);
+        PP_HIP(hipMemcpyAsync(sizes.data(), E->sizes, sizeof(int64_t) * ns, hipMemcpyDeviceToHost, st));
+        PP_HIP(hipStreamSynchronize(st));
+        bool short_of_records = false;
+        for (int i = 0; i < ns && !short_of_records; ++i) short_of_records = sizes[i] < 0;
+        if (short_of_records && rcap < E->full_raw && m > 1) {
+            m = (m + 1) / 2;  // the same frames again, twice the records per slice
+            continue;
+        }
+        int64_t part = 0;
+        for (int f = 0; f < m; ++f) {
+            int64_t fsz = 0;
+            for (int s = 0; s < per; ++s) {
+                const int64_t n = sizes[f * per + s];
+                if (n < 0)
+                    PP_FAIL(PP_ERR_NOMEM, "frame %d slice %d exceeds its %lld-byte buffer", f0 + f, s,
+                            (long long)(rcap * 4));
+                if (n + 8 >= ((int64_t)1 << 24))  // the footer's 24-bit size field (ffv1enc.c asserts the same)
+                    PP_FAIL(PP_ERR_UNSUPPORTED, "frame %d slice %d: %lld bytes exceed the 24-bit slice size", f0 + f,
+                            s, (long long)n);
+                off[f * per + s] = total + part + fsz;
+                fsz += n + 8;
+            }
+            frame_sizes[f0 + f] = fsz;
+            part += fsz;
+        }
+        if (int rc = pk_reserve(E, total + part, total, st)) return rc;
+        PP_HIP(hipMemcpyAsync(E->off, off.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(ffv1_pack_kernel, dim3(ns), dim3(256), 0, st, reinterpret_cast<const uint8_t *>(E->raw),
+                           rcap * 4, E->sizes, E->crcs, E->off, E->pk,
+                           reinterpret_cast<const uint32_t *>(E->tables + 512));
+        PP_HIP(hipGetLastError());
+        // the next launch reuses the records, the sizes and the offsets
+        PP_HIP(hipStreamSynchronize(st));
+        total += part;
+        f0 += m;
     }
+    E->pk_len = total;
+    if (packets) *packets = E->pk;
+    return total;
+}
+
+extern "C" int pp_ffv1_encode_stats(const pp_ffv1_enc *E, int *launches) {
+    if (!E || !launches) PP_FAIL(PP_ERR_INVALID, "null argument");
+    *launches = E->launches;
+    return PP_OK;
+}
+
+extern "C" int64_t pp_ffv1_encode(pp_ffv1_enc *E, const pp_frames *src, int nframes, uint8_t *dst, int64_t dst_cap,
+                                  int64_t *frame_sizes, void *stream) {
+    if (!E || !src || !dst || !frame_sizes || nframes < 0) PP_FAIL(PP_ERR_INVALID, "null argument");
+    const uint8_t *pk = nullptr;
+    const int64_t total = pp_ffv1_encode_packets(E, src, nframes, frame_sizes, &pk, stream);
+    if (total <= 0) return total;
     if (total > dst_cap) PP_FAIL(PP_ERR_NOMEM, "packets need %lld bytes, dst holds %lld", (long long)total, (long long)dst_cap);
-    PP_HIP(hipMemcpyAsync(E->off, off.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(ffv1_pack_kernel, dim3(ns), dim3(256), 0, st, E->slices, E->cap, E->sizes, E->crcs, E->off, dst,
-                       reinterpret_cast<const uint32_t *>(E->tables + 512));
-    PP_HIP(hipGetLastError());
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    PP_HIP(hipMemcpyAsync(dst, pk, total, hipMemcpyDeviceToDevice, st));
     PP_HIP(hipStreamSynchronize(st));
     return total;
 }

@@ -20,61 +20,13 @@
 
 #include "common.hpp"
 #include "device.hpp"
+#include "ffv1host.hpp"
 
 namespace pp {
 
-void rac_states(uint8_t zero[256], uint8_t one[256]);  // ffv1.hip
-void crc_table(uint32_t t[256]);
-
 namespace {
 
-constexpr int kCtx = 32;
-constexpr int kMaxCtx = 4096;              // context count the state blocks are sized for
-
-struct HostRD {
-    int low = 0, range = 0xFF00;
-    const uint8_t *p = nullptr, *end = nullptr;
-    uint8_t zero[256], one[256];
-    HostRD(const uint8_t *b, int64_t n) {
-        rac_states(zero, one);
-        p = b;
-        end = b + n;
-        low = n >= 2 ? (b[0] << 8) | b[1] : 0;
-        p += 2;
-        if (low >= 0xFF00) { low = 0xFF00; end = p; }
-    }
-    void refill() {
-        if (range < 0x100) {
-            range <<= 8;
-            low <<= 8;
-            if (p < end) low += *p++;
-        }
-    }
-    int rac(uint8_t *st) {
-        const int r1 = (range * *st) >> 8;
-        range -= r1;
-        if (low < range) {
-            *st = zero[*st];
-            refill();
-            return 0;
-        }
-        low -= range;
-        *st = one[*st];
-        range = r1;
-        refill();
-        return 1;
-    }
-    int symbol(uint8_t *st) {  // unsigned
-        if (rac(st)) return 0;
-        int e = 0;
-        while (rac(st + 1 + std::min(e, 9))) {
-            if (++e > 31) return -1;
-        }
-        int a = 1;
-        for (int i = e - 1; i >= 0; i--) a += a + rac(st + 22 + std::min(i, 9));
-        return a;
-    }
-};
+constexpr int kCtx = kFfv1CtxBytes;
 
 }  // namespace
 
@@ -277,8 +229,8 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
                 if (neg) ctx = -ctx;
                 const int key = key0 + ctx;
                 if (key != cur_key) {
-                    if (cur_key >= 0 && !(a.debug & 16)) dblk_store(st0 + cur_key * kCtx, blk);
-                    if (!(a.debug & 8)) dblk_load(blk, st0 + key * kCtx);
+                    if (cur_key >= 0 && !(PP_ABLATE(a.debug) & 16)) dblk_store(st0 + cur_key * kCtx, blk);
+                    if (!(PP_ABLATE(a.debug) & 8)) dblk_load(blk, st0 + key * kCtx);
                     cur_key = key;
                 }
                 int diff = dec_symbol<true>(d, blk, s_tab, bad);
@@ -318,64 +270,14 @@ extern "C" int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extra, int ext
     if (!out || !extra) PP_FAIL(PP_ERR_INVALID, "null argument");
     *out = nullptr;
     if (w < 2 || h < 2 || max_frames < 1) PP_FAIL(PP_ERR_INVALID, "bad size %dx%d / max_frames %d", w, h, max_frames);
-    if (extra_size < 8) PP_FAIL(PP_ERR_INVALID, "configuration record of %d bytes", extra_size);
-    {
-        uint32_t t[256];
-        crc_table(t);
-        uint32_t crc = 0;
-        for (int i = 0; i < extra_size; i++) crc = (crc << 8) ^ t[(crc >> 24) ^ extra[i]];
-        if (crc) PP_FAIL(PP_ERR_INVALID, "configuration record CRC mismatch");
-    }
+    Ffv1Record rec;
+    std::string err;
+    if (int rc = ffv1_parse_record(extra, extra_size, w, h, &rec, &err)) PP_FAIL(rc, "%s", err.c_str());
     std::unique_ptr<pp_ffv1_dec> D(new pp_ffv1_dec());
     D->ctx = ctx; D->w = w; D->h = h; D->max_frames = max_frames;
-    HostRD r(extra, extra_size);
-    uint8_t st[kCtx];
-    std::memset(st, 128, sizeof(st));
-    const int version = r.symbol(st);
-    const int micro = r.symbol(st);
-    const int coder = r.symbol(st);
-    const int cs = r.symbol(st);
-    D->bits = r.symbol(st);
-    const int chroma = r.rac(st);
-    D->hsub = r.symbol(st);
-    D->vsub = r.symbol(st);
-    const int alpha = r.rac(st);
-    D->nh = r.symbol(st) + 1;
-    D->nv = r.symbol(st) + 1;
-    const int tables = r.symbol(st);
-    (void)micro;
-    if (version != 3 || coder != 1 || cs != 0 || !chroma || alpha || tables != 1)
-        PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 record: version %d coder %d colorspace %d chroma %d alpha %d tables %d "
-                "(supported: 3, 1, 0, 1, 0, 1)", version, coder, cs, chroma, alpha, tables);
-    if ((D->bits != 8 && D->bits != 10) || D->hsub != 1 || D->vsub > 1)
-        PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 record: %d bits, chroma shifts %d/%d", D->bits, D->hsub, D->vsub);
-    if (D->nh < 1 || D->nv < 1 || D->nh * D->nv > 256 || D->nh > w || D->nv > h)
-        PP_FAIL(PP_ERR_INVALID, "FFV1 record: slice grid %dx%d", D->nh, D->nv);
-    // read_quant_tables: 5 run-length tables; only the first three may vary
-    int cc = 1;
-    for (int t = 0; t < 5; t++) {
-        uint8_t qs[kCtx];
-        std::memset(qs, 128, sizeof(qs));
-        int16_t q[256];
-        int i = 0, v = 0;
-        for (; i < 128; v++) {
-            const int len = r.symbol(qs) + 1;
-            if (len <= 0 || len > 128 - i) PP_FAIL(PP_ERR_INVALID, "FFV1 record: quantisation table %d", t);
-            for (int k = 0; k < len; k++) q[i++] = (int16_t)(cc * v);
-        }
-        for (i = 1; i < 128; i++) q[256 - i] = (int16_t)-q[i];
-        q[128] = (int16_t)-q[127];
-        const int levels = 2 * v - 1;
-        if (t >= 3 && levels != 1) PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 record: 5-input context model");
-        if (t < 3) std::memcpy(D->quant[t], q, sizeof(q));
-        cc *= levels;
-    }
-    D->ctx_count = (cc + 1) / 2;
-    if (D->ctx_count > kMaxCtx) PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 record: %d contexts", D->ctx_count);
-    if (r.rac(st)) PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 record: initial states");
-    D->ec = r.symbol(st);
-    const int intra = r.symbol(st);
-    if (intra != 1) PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 record: inter frames (intra %d)", intra);
+    D->bits = rec.bits; D->hsub = rec.hsub; D->vsub = rec.vsub; D->nh = rec.nh; D->nv = rec.nv; D->ec = rec.ec;
+    D->ctx_count = rec.ctx_count;
+    std::memcpy(D->quant, rec.quant, sizeof(D->quant));
     if (!ctx) {
         *out = D.release();
         return PP_OK;
@@ -429,23 +331,11 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     hipStream_t st = static_cast<hipStream_t>(stream);
     PP_HIP(hipSetDevice(D->ctx->device));
     const int per = D->nh * D->nv, ns = per * nframes;
-    const int trailer = 3 + 5 * (D->ec != 0);
     std::vector<int64_t> soff(ns), slen(ns);
     int64_t base = 0;
-    for (int f = 0; f < nframes; ++f) {  // slices from the end of the packet (ffv1dec.c decode_frame)
-        int64_t end = base + frame_sizes[f];
-        for (int i = per - 1; i >= 0; --i) {
-            if (end - base < trailer) PP_FAIL(PP_ERR_INVALID, "frame %d: slice %d trailer missing", f, i);
-            const uint8_t *t = packets + end - trailer;
-            const int64_t v = ((int64_t)t[0] << 16 | t[1] << 8 | t[2]) + trailer;
-            if (i == 0 ? v != end - base : v > end - base)
-                PP_FAIL(PP_ERR_INVALID, "frame %d: slice pointer chain broken at slice %d", f, i);
-            end -= v;
-            soff[f * per + i] = end;
-            slen[f * per + i] = v;
-        }
-        base += frame_sizes[f];
-    }
+    std::string err;
+    if (int rc = ffv1_slice_table(packets, frame_sizes, nframes, per, D->ec, soff.data(), slen.data(), &base, &err))
+        PP_FAIL(rc, "%s", err.c_str());
     if (base > D->pkt_cap) {
         if (D->pkt) PP_HIP(hipFree(D->pkt));
         D->pkt = nullptr;
@@ -470,7 +360,7 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     a.ctx_count = D->ctx_count; a.state_bytes = sb;
     a.states = D->states; a.status = D->status; a.tables = D->tables; a.quant = D->dquant;
     a.lpw = ffv1_lanes_per_wave(16);
-    if (const char *e = std::getenv("PIXPATH_FFV1_DEBUG")) a.debug = std::atoi(e);
+    if (const char *e = PP_KNOB("PIXPATH_FFV1_DEBUG")) a.debug = std::atoi(e);
     hipLaunchKernelGGL(ffv1_decode_kernel, dim3((ns + a.lpw - 1) / a.lpw), dim3(64), 0, st, a);
     PP_HIP(hipGetLastError());
     std::vector<int> status(ns);

@@ -1,0 +1,48 @@
+// Host side of the FFV1 codec: the range-coder
+// state tables, the CRC, the configuration record (written by the encoder,
+// parsed and checked by the decoder) and the walk of a frame packet's slice
+// footers.  Plain C++ with no HIP dependency, so it also builds on its own
+// under ASan / UBSan (`make sanitize`, csrc/fuzz_host.cpp) and is fuzzed with
+// corrupt records and packets -- every byte it reads comes from a file.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace pp {
+
+constexpr int kFfv1Ctx = 666;   // (11^3 + 1) / 2 contexts of the 3-input set the encoder writes
+constexpr int kFfv1CtxBytes = 32;  // state bytes per context
+constexpr int kFfv1MaxCtx = 4096;  // context count the decoder's state blocks are sized for
+
+// ff_build_rac_states(c, 0.05 * 2^32, 256 - 8): the default state-transition table
+void rac_states(uint8_t zero[256], uint8_t one[256]);
+// AV_CRC_32_IEEE: polynomial 0x04C11DB7, MSB first, initial 0, no final xor
+void crc_table(uint32_t t[256]);
+// the 3-input quantiser the encoder's record describes: min(5, bit length |d|), odd-mirrored
+int ffv1_quant(int i);
+
+// The configuration record (RFC 9043 4.2, ffv1enc.c write_extradata) of
+// pixpath's encoder: version 3, range coder with the default table, one
+// 3-input quantisation set, slice CRCs, intra; CRC-32 parity appended.
+std::vector<uint8_t> ffv1_write_record(int depth, int hsub, int vsub, int slices_h, int slices_v);
+
+// What the decoder needs from a configuration record.
+struct Ffv1Record {
+    int bits = 8, hsub = 1, vsub = 1, nh = 1, nv = 1, ec = 0, ctx_count = 0;
+    int16_t quant[3][256];
+};
+
+// Parse and check a configuration record for a w x h stream: 0 (PP_OK), or a
+// negative PP_ERR_* with *err set.  Never reads outside extra[0, size).
+int ffv1_parse_record(const uint8_t *extra, int size, int w, int h, Ffv1Record *rec, std::string *err);
+
+// The slice table of `nframes` packets held back to back (frame_sizes[f]
+// bytes each): every frame's slice footers walked backwards from the packet
+// end (ffv1dec.c decode_frame), slice i of frame f at soff[f * per + i] with
+// slen bytes (footer included).  0, or a negative PP_ERR_* with *err set.
+int ffv1_slice_table(const uint8_t *packets, const int64_t *frame_sizes, int nframes, int per, int ec,
+                     int64_t *soff, int64_t *slen, int64_t *total, std::string *err);
+
+}  // namespace pp

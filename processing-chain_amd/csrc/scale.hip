@@ -545,7 +545,7 @@ void row_chunks(HostPlane &hp, int sh, int dh, int cho, int seg_h, int *maxnew, 
 
 // LDS budget per workgroup in bytes (PIXPATH_SCALE_LDS_KB overrides, measurement only)
 static size_t lds_budget() {
-    const char *e = std::getenv("PIXPATH_SCALE_LDS_KB");
+    const char *e = PP_KNOB("PIXPATH_SCALE_LDS_KB");
     return e ? (size_t)std::max(8, std::min(160, atoi(e))) * 1024 : (size_t)pp::kLdsBudget;
 }
 
@@ -556,7 +556,7 @@ int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::
     static const int tws[] = {256, 128, 64, 32};
     static const int chos[] = {64, 48, 32, 24, 16, 8, 4, 2, 1};
     // tuning overrides (measurement only): tallest chunk, rows per segment
-    const char *e_cho = std::getenv("PIXPATH_SCALE_CHO_MAX"), *e_seg = std::getenv("PIXPATH_SCALE_SEG_ROWS");
+    const char *e_cho = PP_KNOB("PIXPATH_SCALE_CHO_MAX"), *e_seg = PP_KNOB("PIXPATH_SCALE_SEG_ROWS");
     const int cho_max = e_cho ? std::max(1, atoi(e_cho)) : cho_force > 0 ? cho_force : pp::kChoMax;
     const int seg_rows = seg_force > 0 ? seg_force : e_seg ? std::max(1, atoi(e_seg)) : pp::kSegRows;
     for (int tw : tws) {
@@ -667,6 +667,8 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
     using namespace pp;
     if (!out) PP_FAIL(PP_ERR_INVALID, "null argument");
     *out = nullptr;  // ctx == NULL: host-only plan (tables for introspection, no device upload)
+    const bool force_generic = (flags & PP_PLAN_GENERIC) != 0;
+    flags &= ~PP_PLAN_GENERIC;
     FmtInfo si = fmt_info(src_fmt), di = fmt_info(dst_fmt);
     if (!si.valid || si.packed) PP_FAIL(PP_ERR_INVALID, "source format %d must be planar YUV", src_fmt);
     if (!di.valid || dst_fmt == PP_FMT_V210) PP_FAIL(PP_ERR_INVALID, "destination format %d unsupported", dst_fmt);
@@ -730,7 +732,7 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
         // needs the short chunks; PIXPATH_CHAIN_LUMA_CHO (measurement) sets luma's
         int cho_c = cho_max;
         if (!c && one_seg_chroma)
-            if (const char *e = std::getenv("PIXPATH_CHAIN_LUMA_CHO")) cho_c = std::max(1, atoi(e));
+            if (const char *e = PP_KNOB("PIXPATH_CHAIN_LUMA_CHO")) cho_c = std::max(1, atoi(e));
         if (plan_tiles(hp[c], src_w, src_h, dst_w, dst_h, &P->lds_bytes, &err, c && one_seg_chroma ? 1 << 20 : 0, cho_c))
             PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
     }
@@ -742,9 +744,8 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
     // 1.554 vs 1.501 ms, config 3 10-bit 5.17 vs 4.87 ms, 8-bit 3.57 vs
     // 3.25 ms per 600-frame launch; profiles/r3/strip_tw_ab.txt).
     {
-        const char *force = std::getenv("PIXPATH_SCALE_KERNEL");
-        const char *etw = std::getenv("PIXPATH_STRIP_TW");
-        bool ok0 = !(force && std::strcmp(force, "generic") == 0);
+        const char *etw = PP_KNOB("PIXPATH_STRIP_TW");
+        bool ok0 = !force_generic;
         const int CH = si.depth > 8 ? 8 : 16;
         for (int c = 0; c < 2 && ok0; ++c) ok0 = hp[c].tw == kTileW && hp[c].vtp <= 8;
         const int tw_first = (etw && atoi(etw) == 512 && !one_seg_chroma && !di.packed) ? 512 : 256;
@@ -1073,7 +1074,7 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
     a.dither = allow_dither && P->si.depth > 8 && out_depth == 8;
     a.vec_src = 1;
     a.vec_dst = 1;
-    if (const char *e = std::getenv("PIXPATH_SCALE_DEBUG")) a.debug = atoi(e);
+    if (const char *e = PP_KNOB("PIXPATH_SCALE_DEBUG")) a.debug = atoi(e);
     for (int p = 0; p < 3; ++p) {
         a.vec_src &= aligned(a.src[p], a.sls[p], nframes > 1 ? a.sfs[p] : 0, 16);
         a.vec_dst &= aligned(a.dst[p], a.dls[p], nframes > 1 ? a.dfs[p] : 0, out_depth == 8 ? 4 : 8);
@@ -1170,7 +1171,7 @@ int launch_chain(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, i
     a.dither = P->si.depth > 8;
     a.vec_src = 1;
     a.vec_dst = 1;
-    if (const char *e = std::getenv("PIXPATH_SCALE_DEBUG")) a.debug = atoi(e);
+    if (const char *e = PP_KNOB("PIXPATH_SCALE_DEBUG")) a.debug = atoi(e);
     for (int p = 0; p < 3; ++p)
         a.vec_dst &= aligned(a.dst[p], a.dls[p], nframes > 1 ? a.dfs[p] : 0, P->chain_out == 8 ? 4 : 8);
     const int vtm = strip_vtm_bucket(std::max(P->fjob[0].vtp, P->fjob[1].vtp));

@@ -252,11 +252,11 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
         const int nbase = lo & ~1;
         const int keep = next_src > nbase ? (next_src - nbase + 1) >> 1 : 0;
         const int shift = (nbase - base) >> 1;
-        if (!(a.debug & 8)) __syncthreads();  // staged rows visible; every wave has left the previous V pass
+        if (!(PP_ABLATE(a.debug) & 8)) __syncthreads();  // staged rows visible; every wave has left the previous V pass
         const int after = nnew > 0 ? hi : next_src;
         const bool more = y0 + cho < y_end;
         const int nfrom = more ? max(after, chunk_lo[ci + 1]) : 0, nhi = more ? chunk_hi[ci + 1] : 0;
-        if (more && !(a.debug & 2)) prefetch(pf, nfrom, nhi);
+        if (more && !(PP_ABLATE(a.debug) & 2)) prefetch(pf, nfrom, nhi);
         // kept row pairs move down to the window start, each column by its own
         // lane in increasing order (no lane reads a slot already overwritten)
         bool moved = false;
@@ -278,8 +278,8 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
         if (moved) __syncthreads();
         base = nbase;
         // ---- horizontal pass: row pairs of the window, wave-strided ----------
-        if (nnew > 0 && (a.debug & 4)) next_src = hi;
-        if (nnew > 0 && !(a.debug & 4)) {
+        if (nnew > 0 && (PP_ABLATE(a.debug) & 4)) next_src = hi;
+        if (nnew > 0 && !(PP_ABLATE(a.debug) & 4)) {
             const int i0 = next_src - base;
             const int kf0 = (i0 + 1) >> 1, kf1 = (i0 + nnew) >> 1;
             if ((i0 & 1) && rg == ((i0 >> 1) & 3)) {  // high row of a kept pair
@@ -310,8 +310,8 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
             }
             next_src = hi;
         }
-        if (!(a.debug & 8)) __syncthreads();  // window complete; src_t is free
-        if (more && nhi > nfrom && !(a.debug & 2)) commit(pf, nfrom, nhi);
+        if (!(PP_ABLATE(a.debug) & 8)) __syncthreads();  // window complete; src_t is free
+        if (more && nhi > nfrom && !(PP_ABLATE(a.debug) & 2)) commit(pf, nfrom, nhi);
         // ---- vertical pass: one output row per wave --------------------------
         // raised priority while the wave issues its output rows: the other
         // waves' H pass never starves the write stream (-2 %, profiles/r2)
@@ -370,7 +370,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                         acc[2] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].z), c2, acc[2], false);
                         acc[3] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].w), c2, acc[3], false);
                     }
-                    if (!lane_any || (a.debug & 1)) continue;
+                    if (!lane_any || (PP_ABLATE(a.debug) & 1)) continue;
                     constexpr int sh = OUTB == 8 ? 19 : 11 + 16 - OUTB;
                     constexpr int mx = (1 << OUTB) - 1;
                     int o[4];
@@ -440,7 +440,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
         }
         if constexpr (FUSE >= 8) {
             // ---- second stage (fuse 2): vertical filter of the ring2 rows ----
-            if (J.fuse == 2 && !(a.debug & 16)) {  // debug 16: no second stage (timing only)
+            if (J.fuse == 2 && !(PP_ABLATE(a.debug) & 16)) {  // debug 16: no second stage (timing only)
                 __syncthreads();  // this chunk's first-stage rows are in ring2
                 const int lo2 = chunk2[4 * ci], hi2 = chunk2[4 * ci + 1];
                 const kconst int32_t *vrow2 = as_kconst<int32_t>(J.vrow2);

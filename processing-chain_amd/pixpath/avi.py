@@ -5,7 +5,8 @@ lib/ffmpeg.py:951-954, FFV1 video) when the FFV1 encode runs on the GPU.
 Layout written (RIFF chunks, little-endian):
   RIFF 'AVI ' [ LIST 'hdrl' [ avih, LIST 'strl' [ strh, strf (BITMAPINFOHEADER
   + codec private data), indx (OpenDML super index) ], LIST 'odml' [ dmlh ] ],
-  LIST 'movi' [ '00dc' packets..., ix00 (standard index) ], idx1 ]
+  [ LIST 'INFO' [ ISFT ... ] ], LIST 'movi' [ '00dc' packets..., ix00 (standard
+  index) ], idx1 ]
   RIFF 'AVIX' [ LIST 'movi' [ '00dc'..., ix00 ] ] ...   (every RIFF < 1 GiB)
 The reader walks the chunks (it needs no index).  Round trips are tested
 here; acceptance by FFmpeg's avidec is unpinned (no FFmpeg in this
@@ -25,11 +26,20 @@ def _chunk(fourcc, payload):
 
 
 class AviWriter:
-    def __init__(self, path, w, h, rate, extradata=b"", fourcc=b"FFV1", riff_limit=RIFF_LIMIT):
+    """Writes `path + ".part"` and renames it to `path` on close(): a run that
+    fails (abort(), or an exception before close) never leaves a complete-
+    looking AVI under the output name, which the builders' skip-if-exists rule
+    (`-n`, lib/ffmpeg.py:964-970) would then keep."""
+
+    def __init__(self, path, w, h, rate, extradata=b"", fourcc=b"FFV1", riff_limit=RIFF_LIMIT, info=None):
+        """info: RIFF INFO tags written into the header list (e.g. {b"ISFT":
+        b"pixpath ffv1-gpu 8x8"}, the encoder provenance FFmpeg also writes)."""
         # unbuffered: a packet goes out as one writev of (chunk header, payload,
         # pad) straight from the caller's buffer -- no copy through a Python
         # buffer, and the GIL is released for the whole write
-        self.fh = open(path, "wb", buffering=0)
+        self.path, self.part = path, path + ".part"
+        self.info = dict(info or {})
+        self.fh = open(self.part, "wb", buffering=0)
         self.w, self.h, self.rate = int(w), int(h), Fraction(rate)
         self.extradata, self.fourcc, self.limit = bytes(extradata), fourcc, riff_limit
         self.riffs = []       # per RIFF: [riff_start, movi_start, [(data_offset, size, key)]]
@@ -55,6 +65,9 @@ class AviWriter:
         hdrl = b"hdrl" + _chunk(b"avih", avih) + _chunk(b"LIST", strl) + _chunk(b"LIST", odml)
         self.hdr_start = self.fh.tell()
         self.fh.write(_chunk(b"LIST", hdrl))
+        if self.info:  # LIST 'INFO' (after hdrl, before movi, as avienc.c places it)
+            self.fh.write(_chunk(b"LIST", b"INFO" + b"".join(_chunk(k, bytes(v) + b"\0")
+                                                             for k, v in self.info.items())))
         # offsets of the fields patched on close
         base = self.hdr_start + 12
         self.off_avih = base + 8                               # avih payload
@@ -108,13 +121,54 @@ class AviWriter:
             self._open_movi()
         pos = self.fh.tell()
         parts = [b"00dc" + struct.pack("<I", n), data] + ([b"\0"] if n & 1 else [])
-        total, done = 8 + n + (n & 1), 0
+        total = 8 + n + (n & 1)
+        self._writev(parts, pos, total)
+        self.riffs[-1][2].append((pos + 8, n, key))
+        self.total += 1
+        self.max_size = max(self.max_size, n)
+
+    def write_packets(self, data, sizes):
+        """Append len(sizes) packets held back to back in `data` (bytes-like),
+        with as few writev calls as the iovec limit allows (one Python call
+        per batch of packets instead of per packet)."""
+        data = memoryview(data).cast("B")
+        sizes = [int(n) for n in sizes]
+        i, off = 0, 0
+        while i < len(sizes):
+            start = self.riffs[-1][0]
+            pos = self.fh.tell()
+            parts, ents, total, split = [], [], 0, False
+            # packets of this RIFF segment (the per-packet split rule of write_packet)
+            while i < len(sizes) and len(parts) < 1000:
+                n = sizes[i]
+                if pos + total - start + n + 8 + 16 * (len(self.riffs[-1][2]) + len(ents) + 2) > self.limit \
+                        and (self.riffs[-1][2] or ents):
+                    split = True
+                    break
+                parts.append(b"00dc" + struct.pack("<I", n))
+                parts.append(data[off:off + n])
+                if n & 1:
+                    parts.append(b"\0")
+                ents.append((pos + total + 8, n, True))
+                total += 8 + n + (n & 1)
+                self.max_size = max(self.max_size, n)
+                off += n
+                i += 1
+            if ents:
+                self._writev(parts, pos, total)
+                self.riffs[-1][2].extend(ents)
+                self.total += len(ents)
+            if split:
+                self._close_movi()
+                self._open_movi()
+
+    def _writev(self, parts, pos, total):
+        done = 0
         while done < total:  # writev may write short
             k = os.writev(self.fh.fileno(), parts)
             done += k
             if done < total:
-                self.fh.seek(pos + done)
-                rest, skip = [], done
+                rest, skip = [], k
                 for b in parts:
                     b = memoryview(b).cast("B")
                     if skip >= len(b):
@@ -124,9 +178,6 @@ class AviWriter:
                     skip = 0
                 parts = rest
         self.fh.seek(pos + total)
-        self.riffs[-1][2].append((pos + 8, n, key))
-        self.total += 1
-        self.max_size = max(self.max_size, n)
 
     def close(self):
         self._close_movi()
@@ -149,6 +200,15 @@ class AviWriter:
             self.fh.write(struct.pack("<QII", ix_pos, ix_size, len(ents)))
             self.fh.seek(cur)
         self.fh.close()
+        os.replace(self.part, self.path)
+
+    def abort(self):
+        """Drop the partial output (the output name is never created)."""
+        try:
+            self.fh.close()
+        finally:
+            if os.path.exists(self.part):
+                os.remove(self.part)
 
 
 def scan(path):
@@ -191,6 +251,9 @@ def scan(path):
                         d = fh.read(size)
                         bi_size, w, h = struct.unpack_from("<Iii", d, 0)
                         info.update(w=w, h=abs(h), fourcc=d[16:20], extradata=d[40:bi_size])
+                elif tag in (b"ISFT", b"ICMT") and tag not in info.get("tags", {}):
+                    fh.seek(body)
+                    info.setdefault("tags", {})[tag] = fh.read(size).rstrip(b"\0")
                 elif tag[2:] in (b"dc", b"db") and tag[:2].isdigit():
                     if state["video"] is not None and int(tag[:2]) == state["video"]:
                         index.append((body, size))

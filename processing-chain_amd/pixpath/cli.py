@@ -11,6 +11,7 @@ the ffmpeg strings they replace).
   stall  AVPVS -> stall frames (frozen/black + spinner) or frame freezing
          (bufferer call p03_generateAvPvs.py:236-243, spec PP-STALL-1)
   concat long-test segment AVIs -> one AVI, packets copied (create_avpvs_long_concat :1058, GPU-FFV1 AVIs)
+  preview AVPVS decoded here (GPU FFV1) -> ffmpeg's ProRes (create_preview :1250)
   siti   P.910 SI/TI of a SRC (util/SRC_analysis.py hook)
 
 Inputs/outputs ending in .y4m or .raw/.yuv are read/written directly;
@@ -136,8 +137,8 @@ def cmd_avpvs(args):
     dev = _device()
     torch.cuda.set_device(dev)
     if args.ffv1_input:  # an AVPVS written by `--gpu-ffv1` (mobile CPVS scale reads it)
-        from .ffv1 import Ffv1AviReader
-        rd = Ffv1AviReader(args.input, device=dev)
+        from .ffv1 import open_avpvs_reader
+        rd = open_avpvs_reader(args.input, device=dev)
     else:
         rd = pio.open_reader(args.input)
     W, H = (int(v) for v in args.size.split("x"))
@@ -157,7 +158,8 @@ def cmd_avpvs(args):
         # the AVPVS as FFV1 encoded on the GPU, in an AVI written here (video
         # only: the reference's -c:a flac track needs ffmpeg, see _mux_audio)
         from .ffv1 import Ffv1AviWriter
-        inner = Ffv1AviWriter(out, target, W, H, rate, device=dev)
+        sl = tuple(int(v) for v in args.ffv1_slices.lower().split("x")) if args.ffv1_slices else None
+        inner = Ffv1AviWriter(out, target, W, H, rate, slices=sl, device=dev)
     else:
         inner = _open_writer(out, target, W, H, rate, args.vopts, args.aopts,
                              None if args.aopts.strip() == "-an" else args.input, args.y)
@@ -310,8 +312,8 @@ def cmd_cpvs(args):
     dev = _device()
     torch.cuda.set_device(dev)
     if args.gpu_ffv1:  # an FFV1 AVPVS written by `avpvs --gpu-ffv1`: decoded on the GPU
-        from .ffv1 import Ffv1AviReader
-        rd = Ffv1AviReader(args.input, device=dev)
+        from .ffv1 import open_avpvs_reader
+        rd = open_avpvs_reader(args.input, device=dev)
     else:
         rd = pio.open_reader(args.input)
     W, H = (rd.w, rd.h) if not args.pad else (int(v) for v in args.pad.split("x"))
@@ -508,17 +510,17 @@ def cmd_stall(args):
     torch.cuda.set_device(dev)
     gpu_out = getattr(args, "gpu_ffv1_out", args.gpu_ffv1)
     if args.gpu_ffv1 and gpu_out:
-        from .ffv1 import Ffv1AviReader, stall_avi
+        from .ffv1 import open_avpvs_reader, stall_avi
         events = ast.literal_eval(args.buffer)
         n = stall_avi(args.input, out, events, args.skipping, args.spinner, args.black_frame, dev)
         if n is not None:  # packet level: copied input packets + encoded stall frames
             from .avi import scan
             _mux_stall_audio(out, args.input, args.aopts, events, args.skipping, scan(args.input)[0]["rate"])
             return 0
-        rd = Ffv1AviReader(args.input, device=dev)
+        rd = open_avpvs_reader(args.input, device=dev)  # not pixpath's FFV1: decode it (GPU or ffmpeg)
     elif args.gpu_ffv1:
-        from .ffv1 import Ffv1AviReader
-        rd = Ffv1AviReader(args.input, device=dev)
+        from .ffv1 import open_avpvs_reader
+        rd = open_avpvs_reader(args.input, device=dev)
     else:
         rd = pio.open_reader(args.input)
     so = _StallOutput(out, rd.fmt, rd.w, rd.h, rd.rate, args.buffer, args.skipping, args.spinner, args.black_frame,
@@ -566,16 +568,47 @@ def cmd_concat(args):
                 (info["w"], info["h"], info["rate"]) != (i0["w"], i0["h"], i0["rate"]):
             raise SystemExit("pixpath concat: %s is not a GPU-FFV1 AVI matching %s" % (f, files[0]))
     cap = int(round(Fraction(str(args.duration)) * i0["rate"])) if args.duration else None
-    wr = avi.AviWriter(out, i0["w"], i0["h"], i0["rate"], extradata=i0["extradata"])
+    wr = avi.AviWriter(out, i0["w"], i0["h"], i0["rate"], extradata=i0["extradata"], info=i0.get("tags"))
     n = 0
-    for f, (_, index) in zip(files, scans):
-        with open(f, "rb") as fh:
-            for off, size in index:
-                if cap is not None and n >= cap:
-                    break
-                fh.seek(off)
-                wr.write_packet(fh.read(size))
-                n += 1
+    try:
+        for f, (_, index) in zip(files, scans):
+            with open(f, "rb") as fh:
+                for off, size in index:
+                    if cap is not None and n >= cap:
+                        break
+                    fh.seek(off)
+                    wr.write_packet(fh.read(size))
+                    n += 1
+    except BaseException:
+        wr.abort()
+        raise
+    wr.close()
+    return 0
+
+
+def cmd_preview(args):
+    """create_preview (lib/ffmpeg.py:1250-1259: `ffmpeg -i <avpvs> -c:v prores
+    -c:a aac <preview>`) with the AVPVS decoded here -- on the GPU when it is
+    pixpath's FFV1 -- and piped to ffmpeg's ProRes encoder with the AVPVS's
+    audio; no pixel work besides the decode."""
+    import torch
+    out = args.output
+    if _skip(out, args.y):
+        return 0
+    dev = _device()
+    torch.cuda.set_device(dev)
+    from .ffv1 import open_avpvs_reader
+    rd = open_avpvs_reader(args.input, device=dev)
+    wr = _open_writer(out, rd.fmt, rd.w, rd.h, rd.rate, args.vopts, args.aopts, args.input, args.y)
+    B = max(1, int(args.batch))
+    buf = np.empty((B, rd.frame_bytes), np.uint8)
+    while True:
+        k = rd.read_into(buf, B)
+        if k:
+            wr.write(buf[:k])
+        if k < B:
+            break
+    rd.close()
     wr.close()
     return 0
 
@@ -635,6 +668,7 @@ def main(argv=None):
     p.add_argument("--stall-vopts", default="-c:v ffv1")
     p.add_argument("--stall-aopts", default="-c:a pcm_s16le")
     p.add_argument("--gpu-ffv1", action="store_true", help="FFV1 encoded on the GPU into an AVI (pixpath.avi)")
+    p.add_argument("--ffv1-slices", default=None, help="slice grid HxV of the GPU FFV1 (default PIXPATH_FFV1_SLICES, 8x8)")
     p.add_argument("--ffv1-input", action="store_true", help="input is a --gpu-ffv1 AVI: decode it on the GPU")
     p.set_defaults(fn=cmd_avpvs)
 
@@ -679,6 +713,10 @@ def main(argv=None):
     p.add_argument("--duration", default=None)
     p.add_argument("output")
     p.set_defaults(fn=cmd_concat)
+
+    p = sub.add_parser("preview")
+    common(p)
+    p.set_defaults(fn=cmd_preview)
 
     p = sub.add_parser("siti")
     p.add_argument("--input", required=True)

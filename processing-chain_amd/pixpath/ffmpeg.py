@@ -12,9 +12,12 @@ PIXPATH_BACKEND:
 * "gpu": the pixel work of a builder runs on the MI355X through
   ``python3 -m pixpath.cli`` (ffmpeg still decodes and encodes; frames cross
   PCIe once each way and every filter between decode and encode runs as HIP
-  kernels).  Builders without pixel work (stream-copy concat, audio mux,
-  preview) keep their ffmpeg strings; the mobile/tablet CPVS run their scale on
-  the MI355X and keep x264 (the tablet pad branch keeps the reference's string).
+  kernels).  The AVPVS intermediate is FFV1 coded on the GPU (PIXPATH_FFV1,
+  default "gpu"; "ffmpeg" keeps the reference's `-coder 1 -context 1` encoder,
+  the reference-faithful bitstream): then the long-test concat copies packets
+  and the preview decodes on the GPU.  The audio mux stays a stream copy by
+  ffmpeg; the mobile/tablet CPVS run their scale on the MI355X and keep x264
+  (the tablet pad branch keeps the reference's string).
 
 Reference functions mirrored (file:line in pnats2avhd/processing-chain):
   calculate_avpvs_video_dimensions  lib/ffmpeg.py:33
@@ -79,13 +82,26 @@ def ffv1_on_gpu():
     return v == "gpu"
 
 
+def ffv1_slices():
+    """The GPU FFV1 slice grid "HxV" (PIXPATH_FFV1_SLICES, default 8x8)."""
+    v = os.environ.get("PIXPATH_FFV1_SLICES", "8x8").lower()
+    t = v.split("x")
+    if len(t) != 2 or not all(x.isdigit() and int(x) > 0 for x in t):
+        raise ValueError("PIXPATH_FFV1_SLICES must be HxV, e.g. 16x16")
+    return v
+
+
 def _gpu_cli(sub, args):
     args = list(args)
     if ffv1_on_gpu():
         # FFV1 AVPVS coded on the GPU in pixpath's own AVI: the AVPVS writers
-        # encode it, its readers (CPVS, stall, mobile scale) decode it there
+        # encode it, its readers (CPVS, stall, mobile scale) decode it there.
+        # The codec and slice grid are part of the command, so p03's per-PVS
+        # log (`ffmpegCommand:` lines, p03_generateAvPvs.py:41-59) records them;
+        # with PIXPATH_FFV1=ffmpeg the command carries the reference's
+        # `-c:v ffv1 ... -coder 1 -context 1` options instead.
         if sub == "avpvs" and FFV1_OPTS in args:
-            args.insert(-1, "--gpu-ffv1")
+            args[-1:-1] = ["--gpu-ffv1", "--ffv1-slices", ffv1_slices()]
         elif sub == "avpvs":
             args.insert(-1, "--ffv1-input")
         elif sub in ("cpvs", "stall"):
@@ -432,7 +448,17 @@ def create_cpvs(pvs, post_processing, rawvideo=False, overwrite=False, nonraw_cr
 
 
 def create_preview(pvs, overwrite=False):
-    """ProRes preview (lib/ffmpeg.py:1250-1259); codec work, ffmpeg in both backends."""
+    """ProRes preview (lib/ffmpeg.py:1250-1259).  The encode is codec work
+    (ffmpeg's ProRes in both backends); with the GPU FFV1 AVPVS the gpu backend
+    decodes the AVPVS on the GPU (`pixpath.cli preview`) and pipes the frames
+    to that encoder, so FFmpeg never decodes pixpath's FFV1 bitstream."""
+    if _backend == "gpu" and ffv1_on_gpu():
+        output_file = pvs.get_preview_file_path()
+        overwrite_spec, skip = _skip_existing(output_file, overwrite)
+        if skip:
+            return None
+        return _collapse(_gpu_cli("preview", [overwrite_spec, "--input", pvs.get_avpvs_file_path(), "--vopts",
+                                              "-c:v prores", "--aopts", "-c:a aac", output_file]))
     return simple_encoding(pvs, overwrite, pvs.get_avpvs_file_path(), pvs.get_preview_file_path(), "-c:v prores",
                            "-c:a aac")
 

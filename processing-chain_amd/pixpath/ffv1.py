@@ -9,6 +9,7 @@ Bitstream choices that differ from ffmpeg's encoder and the parity status
 CPU restatement oracle/ffv1_oracle.c decodes it losslessly) are in DESIGN.md.
 """
 import ctypes
+import os
 import queue
 import threading
 
@@ -16,7 +17,7 @@ import numpy as np
 import torch
 
 from . import formats
-from ._native import check, lib
+from ._native import PP_COPY_D2D, PP_COPY_D2H, check, lib
 from .ops import _stream, context
 
 
@@ -31,7 +32,7 @@ class Ffv1Encoder:
         check(lib().pp_ffv1_encoder_create(None if host_only else self.ctx.handle, self.fmt.id, self.w, self.h,
                                            self.slices[0], self.slices[1], self.max_frames, ctypes.byref(h_)))
         self.handle = h_
-        self._out = None
+        self.stages = None  # the AVI writer's staging batches, pooled with the encoder
 
     def __del__(self):
         if getattr(self, "handle", None):
@@ -49,33 +50,59 @@ class Ffv1Encoder:
         check(lib().pp_ffv1_extradata(self.handle, buf, n))
         return bytes(buf)
 
+    @property
+    def memory_bytes(self):
+        """Device bytes this encoder holds (tokens, records, context states, packets)."""
+        v = ctypes.c_int64()
+        check(lib().pp_ffv1_encoder_memory(self.handle, ctypes.byref(v)))
+        return v.value
+
+    @property
+    def launches(self):
+        """Launches of the last encode: 1, or more when a slice needed more
+        renorm records than the per-slice budget and the batch was re-coded
+        in halves (pp_ffv1_encode_packets)."""
+        v = ctypes.c_int()
+        check(lib().pp_ffv1_encode_stats(self.handle, ctypes.byref(v)))
+        return v.value
+
+    def encode_packets(self, src, stream=None):
+        """Encode a FrameBatch into the encoder's own device packet buffer:
+        (device pointer, total bytes, numpy int64 frame sizes).  The packets
+        are valid until the next encode.  Synchronises the stream."""
+        if (src.fmt.id, src.w, src.h) != (self.fmt.id, self.w, self.h):
+            raise ValueError("batch does not match the encoder")
+        sizes = np.zeros(src.n, np.int64)
+        s = src.frames_struct()
+        ptr = ctypes.c_void_p()
+        total = check(lib().pp_ffv1_encode_packets(self.handle, ctypes.byref(s), src.n,
+                                                   sizes.ctypes.data_as(ctypes.c_void_p), ctypes.byref(ptr),
+                                                   _stream(src.planes[0], stream)))
+        return ptr.value, total, sizes
+
     def encode(self, src, stream=None):
         """Encode a FrameBatch; returns (device uint8 tensor of the packets back to back,
         numpy int64 frame sizes).  Synchronises the stream."""
-        if (src.fmt.id, src.w, src.h) != (self.fmt.id, self.w, self.h):
-            raise ValueError("batch does not match the encoder")
-        raw = sum(src.view(p)[0].numel() * src.view(p).element_size() for p in range(3))
-        cap = src.n * (raw * 3 // 2 + 4096 + 64 * self.slices[0] * self.slices[1])
-        if self._out is None or self._out.numel() < cap:
-            self._out = torch.empty(cap, dtype=torch.uint8, device=src.device)
-        sizes = np.zeros(src.n, np.int64)
-        s = src.frames_struct()
-        total = check(lib().pp_ffv1_encode(self.handle, ctypes.byref(s), src.n,
-                                           ctypes.c_void_p(self._out.data_ptr()), cap,
-                                           sizes.ctypes.data_as(ctypes.c_void_p), _stream(src.planes[0], stream)))
-        return self._out[:total], sizes
+        ptr, total, sizes = self.encode_packets(src, stream)
+        out = torch.empty(max(total, 1), dtype=torch.uint8, device=src.device)
+        if total:
+            st = _stream(src.planes[0], stream)
+            check(lib().pp_copy_async(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ptr), total, PP_COPY_D2D, st))
+            check(lib().pp_stream_synchronize(st))
+        return out[:total], sizes
 
     def encode_host(self, src, stream=None):
         """(numpy uint8 view of the packets in a pinned host buffer, frame sizes):
-        encode, then one D2H of the packets (valid until the next call)."""
-        buf, sizes = self.encode(src, stream)
-        n = buf.numel()
+        encode, then one D2H of the packets straight from the encoder's packet
+        buffer (valid until the next call)."""
+        ptr, n, sizes = self.encode_packets(src, stream)
         if getattr(self, "_host", None) is None or self._host.numel() < n:
-            self._host = torch.empty(max(n, 1 << 20), dtype=torch.uint8).pin_memory()
-        st = torch.cuda.current_stream(src.device) if stream is None else stream
-        with torch.cuda.stream(st):
-            self._host[:n].copy_(buf, non_blocking=True)
-        st.synchronize()
+            self._host = torch.empty(max(n + n // 4, 1 << 20), dtype=torch.uint8).pin_memory()
+        if n:
+            st = _stream(src.planes[0], stream)
+            check(lib().pp_copy_async(ctypes.c_void_p(self._host.data_ptr()), ctypes.c_void_p(ptr), n, PP_COPY_D2H,
+                                      st))
+            check(lib().pp_stream_synchronize(st))
         return self._host[:n].numpy(), sizes
 
     def encode_to_host(self, src, stream=None):
@@ -101,13 +128,17 @@ _POOL_LOCK = threading.Lock()
 _POOL = {}  # (fmt, w, h, slices, max_frames, device) -> [idle Ffv1Encoder]
 
 
+def _pool_key(fmt, w, h, slices, max_frames, device):
+    return (formats.fmt(fmt).id, int(w), int(h), tuple(int(v) for v in slices), int(max_frames), int(device))
+
+
 def acquire_encoder(fmt, w, h, slices=(8, 8), max_frames=600, device=None):
     """An idle encoder of this geometry from the process's pool, else a new
-    one.  An encoder holds ~20 GB of HBM for a 600-frame 1080p batch (tokens,
-    records, slice buffers, context states); consecutive PVSes of one process
-    reuse it instead of allocating and freeing it per PVS."""
-    key = (formats.fmt(fmt).id, int(w), int(h), tuple(int(v) for v in slices), int(max_frames),
-           context(device).device)
+    one.  An encoder of a 600-frame 1080p yuv422p10le batch holds ~17 GB of
+    HBM (tokens 10 GB, renorm records 5 GB, context states 1.6 GB, packets),
+    plus the writer's staging batch (5 GB) that is pooled with it; consecutive
+    PVSes of one process reuse them instead of allocating per PVS."""
+    key = _pool_key(fmt, w, h, slices, max_frames, context(device).device)
     with _POOL_LOCK:
         idle = _POOL.get(key)
         if idle:
@@ -115,11 +146,46 @@ def acquire_encoder(fmt, w, h, slices=(8, 8), max_frames=600, device=None):
     return Ffv1Encoder(fmt, w, h, slices=slices, max_frames=max_frames, device=device)
 
 
-def release_encoder(enc):
-    """Return an encoder from acquire_encoder() to the pool."""
-    key = (enc.fmt.id, enc.w, enc.h, enc.slices, enc.max_frames, enc.ctx.device)
+def release_encoder(enc, ok=True):
+    """Return an encoder from acquire_encoder() to the pool; one that failed
+    mid-encode (ok=False) is freed instead."""
+    if not ok:
+        enc.stages = None
+        return
+    key = _pool_key(enc.fmt, enc.w, enc.h, enc.slices, enc.max_frames, enc.ctx.device)
     with _POOL_LOCK:
         _POOL.setdefault(key, []).append(enc)
+
+
+def reserve_encoders(fmt, w, h, count, slices=(8, 8), max_frames=600, device=None, stages=1):
+    """Make the pool hold at least `count` idle encoders of this geometry, each
+    with `stages` staging batches -- the writers of that many PVSes in flight
+    then allocate nothing (`cli` and the bench call this before their first
+    PVS).  Returns the number created."""
+    from .frames import FrameBatch
+    key = _pool_key(fmt, w, h, slices, max_frames, context(device).device)
+    with _POOL_LOCK:
+        have = len(_POOL.get(key, []))
+    made = []
+    for _ in range(max(0, count - have)):
+        made.append(Ffv1Encoder(fmt, w, h, slices=slices, max_frames=max_frames, device=device))
+    with _POOL_LOCK:
+        idle = _POOL.setdefault(key, [])
+        idle.extend(made)
+        encs = list(idle)
+    for enc in encs:
+        st = getattr(enc, "stages", None) or []
+        while len(st) < stages:
+            st.append(FrameBatch.interleaved(enc.fmt, enc.w, enc.h, enc.max_frames,
+                                             device=torch.device("cuda", enc.ctx.device)))
+        enc.stages = st
+    return len(made)
+
+
+def clear_pool():
+    """Free every idle pooled encoder (and its staging batches)."""
+    with _POOL_LOCK:
+        _POOL.clear()
 
 
 class Ffv1Decoder:
@@ -166,6 +232,12 @@ class Ffv1Decoder:
         return dst
 
 
+def provenance(slices):
+    """The encoder tag written into the AVPVS (RIFF INFO ISFT) and echoed in
+    the GPU command string p03 logs as `ffmpegCommand:` (p03_generateAvPvs.py:41-59)."""
+    return "pixpath ffv1-gpu v3 intra %dx%d slices" % (int(slices[0]), int(slices[1]))
+
+
 class Ffv1AviWriter:
     """`cli avpvs --gpu-ffv1`: the AVPVS written as FFV1 encoded on the GPU in
     an AVI (pixpath.avi) -- the `-c:v ffv1 ... <pvs>.avi` of lib/ffmpeg.py:993
@@ -175,14 +247,17 @@ class Ffv1AviWriter:
     (``write_device``: no D2H, no re-upload) or from host frames (``write``) --
     into batches of ``batch`` frames (default 600, a 10 s PVS at 60 fps: the
     encoder's parallelism is frames x slices).  A full batch is encoded by a
-    worker thread on its own stream while the next batch fills (two staging
-    batches), its packets come back in one pinned D2H and go into the AVI."""
+    worker thread on its own stream while the next batch fills (a second
+    staging batch, allocated only when a PVS has more than one batch), its
+    packets come back in one pinned D2H and go into the AVI.  The encoder and
+    its staging batches come from the process's pool (acquire_encoder)."""
 
     def __init__(self, path, fmt, w, h, rate, slices=None, batch=600, device=None):
         """slices: the FFV1 slice grid (default PIXPATH_FFV1_SLICES, else 8x8;
         16x16 encodes ~1.3x faster at ~7 % larger files)."""
+        import time
         from . import avi
-        from .frames import FrameBatch
+        t0 = time.perf_counter()
         if slices is None:
             slices = default_slices()
         self.fmt = formats.fmt(fmt)
@@ -191,7 +266,9 @@ class Ffv1AviWriter:
         self.batch = int(batch)
         self.enc = acquire_encoder(self.fmt, w, h, slices=slices, max_frames=self.batch, device=device)
         self.device = torch.device("cuda", self.enc.ctx.device)
-        self.stages = [FrameBatch.interleaved(self.fmt, w, h, self.batch, device=self.device) for _ in range(2)]
+        if self.enc.stages is None:
+            self.enc.stages = []
+        self._stage(0)
         self.free = [threading.Event(), threading.Event()]
         for e in self.free:
             e.set()
@@ -199,39 +276,53 @@ class Ffv1AviWriter:
         self.free[0].clear()
         self.stream = torch.cuda.Stream(self.device)
         self.put_stream = torch.cuda.Stream(self.device)  # host-frame uploads
-        self.avi = avi.AviWriter(path, w, h, rate, extradata=self.enc.extradata)
+        self.avi = avi.AviWriter(path, w, h, rate, extradata=self.enc.extradata,
+                                 info={b"ISFT": provenance(self.enc.slices).encode()})
         self.frames = 0
-        self.stats = {"encode_s": 0.0, "write_s": 0.0, "bytes": 0}  # worker-thread time per part
+        # worker-thread time per part; setup_s: encoder + staging + file open (0 allocations when pooled)
+        self.stats = {"encode_s": 0.0, "write_s": 0.0, "bytes": 0, "launches": 0,
+                      "setup_s": time.perf_counter() - t0, "timeline": []}
         self.last_stream = self.put_stream
         self.q = queue.Queue()
         self.err = []
         self.th = threading.Thread(target=self._work, daemon=True)
         self.th.start()
 
+    def _stage(self, k):
+        from .frames import FrameBatch
+        st = self.enc.stages
+        while len(st) <= k:
+            st.append(FrameBatch.interleaved(self.fmt, self.w, self.h, self.batch, device=self.device))
+        return st[k]
+
     def _work(self):
+        import time
         from .frames import FrameBatch
         while True:
             item = self.q.get()
             if item is None:
                 return
-            slot, n, ev = item
+            slot, n, ev, t_q = item
             try:
                 if not self.err:
+                    t_w = time.perf_counter()
                     self.stream.wait_event(ev)
+                    ev.synchronize()  # the frames of this batch are in the staging batch
                     src = FrameBatch.interleaved(self.fmt, self.w, self.h, n, device=self.device,
-                                                 storage=self.stages[slot].storage[:n])
-                    import time
+                                                 storage=self.enc.stages[slot].storage[:n])
                     t0 = time.perf_counter()
                     with torch.cuda.stream(self.stream):
                         data, sizes = self.enc.encode_host(src, stream=self.stream)
                     t1 = time.perf_counter()
-                    off = 0
-                    for k in sizes.tolist():
-                        self.avi.write_packet(data[off:off + k])
-                        off += k
+                    self.avi.write_packets(data, sizes)
+                    t2 = time.perf_counter()
                     self.stats["encode_s"] += t1 - t0
-                    self.stats["write_s"] += time.perf_counter() - t1
-                    self.stats["bytes"] += off
+                    self.stats["write_s"] += t2 - t1
+                    self.stats["bytes"] += int(sizes.sum())
+                    self.stats["launches"] += self.enc.launches
+                    # timeline (perf_counter): batch queued, worker picked it up,
+                    # its frames ready on the GPU, packets on the host, packets written
+                    self.stats["timeline"].append((t_q, t_w, t0, t1, t2))
             except Exception as e:  # surfaced by the next write / close
                 self.err.append(e)
             finally:
@@ -242,9 +333,10 @@ class Ffv1AviWriter:
             raise self.err[0]
 
     def _submit(self, stream):
+        import time
         ev = torch.cuda.Event()
         ev.record(stream)
-        self.q.put((self.cur, self.fill, ev))
+        self.q.put((self.cur, self.fill, ev, time.perf_counter()))
         self.cur ^= 1
         self.free[self.cur].wait()
         self.free[self.cur].clear()
@@ -256,8 +348,9 @@ class Ffv1AviWriter:
         k, i = rows.shape[0], 0
         while i < k:
             take = min(k - i, self.batch - self.fill)
+            stage = self._stage(self.cur)
             with torch.cuda.stream(stream):
-                self.stages[self.cur].storage[self.fill:self.fill + take].copy_(rows[i:i + take], non_blocking=True)
+                stage.storage[self.fill:self.fill + take].copy_(rows[i:i + take], non_blocking=True)
             self.fill += take
             self.frames += take
             i += take
@@ -299,26 +392,35 @@ class Ffv1AviWriter:
             d = torch.from_numpy(data[:n * self.fb].reshape(n, self.fb)).to(self.device, non_blocking=False)
         self._put(d, self.put_stream)
 
-    def release(self):
-        """After close(): the encoder goes back to the pool, the staging batches are dropped."""
+    def release(self, ok=True):
+        """After close(): the encoder and its staging batches go back to the
+        pool (freed instead when the encode failed)."""
         if self.enc is not None:
-            release_encoder(self.enc)
+            release_encoder(self.enc, ok=ok)
         self.enc = None
-        self.stages = None
 
     def close(self):
+        """Encode what is left, finish the AVI and rename it into place; on any
+        failure the partial file is removed and the error re-raised."""
+        ok = False
         try:
             if self.fill:
+                import time
                 ev = torch.cuda.Event()
                 ev.record(self.last_stream)
-                self.q.put((self.cur, self.fill, ev))
+                self.q.put((self.cur, self.fill, ev, time.perf_counter()))
                 self.fill = 0
             self.q.put(None)
             self.th.join()
             self._check()
-        finally:
             self.avi.close()
-            self.release()
+            ok = True
+            import time
+            self.stats["closed_at"] = time.perf_counter()
+        finally:
+            if not ok:
+                self.avi.abort()
+            self.release(ok)
 
 
 class Ffv1AviReader:
@@ -328,11 +430,12 @@ class Ffv1AviReader:
     from the file when that batch is decoded, so a long-test AVPVS of tens of
     GB never sits in host memory."""
 
-    def __init__(self, path, batch=600, device=None):
+    def __init__(self, path, batch=600, device=None, scanned=None):
         """batch: frames decoded per launch (the decoder's parallelism is
-        frames x slices, so a whole 10-s PVS at once)."""
+        frames x slices, so a whole 10-s PVS at once); scanned: avi.scan(path)
+        when the caller already has it."""
         from . import avi
-        info, self.index = avi.scan(path)
+        info, self.index = scanned if scanned is not None else avi.scan(path)
         if info.get("fourcc") != b"FFV1":
             raise ValueError("%s: not an FFV1 AVI" % path)
         self.w, self.h, self.rate = info["w"], info["h"], info["rate"]
@@ -415,6 +518,37 @@ class Ffv1AviReader:
         self.fh.close()
 
 
+def is_pixpath_ffv1(info):
+    """True when an AVI's video stream (avi.scan info) is FFV1 with exactly the
+    configuration record pixpath's encoder writes for its format, size and
+    slice grid -- the streams the GPU decoder reads.  FFmpeg's own FFV1
+    (`-coder 1 -context 1`: custom state table, 5-input contexts, inter
+    frames) is not, and neither is any other record."""
+    from ._native import PixpathError
+    if info.get("fourcc") != b"FFV1" or not info.get("extradata") or "w" not in info:
+        return False
+    try:
+        dec = Ffv1Decoder(info["extradata"], info["w"], info["h"], max_frames=1, host_only=True)
+        probe = Ffv1Encoder(dec.fmt, info["w"], info["h"], slices=dec.slices, host_only=True)
+    except (PixpathError, ValueError):
+        return False
+    return probe.extradata == info["extradata"]
+
+
+def open_avpvs_reader(path, device=None, batch=600):
+    """The reader of an AVPVS: the GPU FFV1 decoder (Ffv1AviReader) for an AVI
+    pixpath's encoder wrote, else ffmpeg's decoder through pixpath.io (an
+    AVPVS from the reference, from a PIXPATH_FFV1=ffmpeg run, or one kept by
+    the `-n` skip rule)."""
+    from . import avi, io as pio
+    scanned = None
+    if path.lower().endswith(".avi") and os.path.isfile(path):
+        scanned = avi.scan(path)
+        if is_pixpath_ffv1(scanned[0]):
+            return Ffv1AviReader(path, batch=batch, device=device, scanned=scanned)
+    return pio.open_reader(path)
+
+
 def stall_avi(src_path, dst_path, buffer_events, skipping, spinner_path=None, black_frame=True, device=None):
     """PP-STALL-1 (the bufferer step, p03_generateAvPvs.py:236-243) on an
     all-intra FFV1 AVI written by Ffv1AviWriter, at the PACKET level: every
@@ -428,13 +562,10 @@ def stall_avi(src_path, dst_path, buffer_events, skipping, spinner_path=None, bl
     from . import avi, ops, spinner, stall
     from .frames import FrameBatch
     info, index = avi.scan(src_path)
-    if info.get("fourcc") != b"FFV1":
+    if not is_pixpath_ffv1(info):
         return None
     rate, w, h = info["rate"], info["w"], info["h"]
     dec = Ffv1Decoder(info["extradata"], w, h, max_frames=1, device=device)
-    enc_probe = Ffv1Encoder(dec.fmt, w, h, slices=dec.slices, host_only=True)
-    if enc_probe.extradata != info["extradata"]:
-        return None
     delays = None
     if not skipping:
         anim, delays = spinner.load_apng(spinner_path)
@@ -456,26 +587,41 @@ def stall_avi(src_path, dst_path, buffer_events, skipping, spinner_path=None, bl
                 pk = packet(s)
                 dec.decode(pk, [len(pk)], dst=FrameBatch.interleaved(dec.fmt, w, h, 1, device=dev,
                                                                       storage=sb.storage[k:k + 1]))
-            B = min(600, len(compose))
-            enc = Ffv1Encoder(dec.fmt, w, h, slices=dec.slices, max_frames=B, device=dev)
-            out = FrameBatch.interleaved(dec.fmt, w, h, B, device=dev)
-            for i in range(0, len(compose), B):
-                part = compose[i:i + B]
-                m = len(part)
-                dst = FrameBatch.interleaved(dec.fmt, w, h, m, device=dev, storage=out.storage[:m])
-                ops.stall_compose(sb, [pos[s] if s >= 0 else -1 for s, _ in part], [sp for _, sp in part], dst=dst)
-                data, sizes = enc.encode_host(dst)
-                o = 0
-                for k in sizes.tolist():
-                    packets.append(data[o:o + k].tobytes())
-                    o += k
-        wr = avi.AviWriter(dst_path, w, h, rate, extradata=info["extradata"])
-        j = 0
-        for s, sp in seq:
-            if sp >= 0 or s < 0:
-                wr.write_packet(packets[j])
-                j += 1
-            else:
-                wr.write_packet(packet(s))
+            # the process's pooled 600-frame encoder (the AVPVS writer's, when the
+            # stall pass follows it in the same process) and its staging batch
+            B = 600
+            enc = acquire_encoder(dec.fmt, w, h, slices=dec.slices, max_frames=B, device=dev.index)
+            ok = False
+            try:
+                if not enc.stages:
+                    enc.stages = [FrameBatch.interleaved(dec.fmt, w, h, B, device=dev)]
+                out = enc.stages[0]
+                for i in range(0, len(compose), B):
+                    part = compose[i:i + B]
+                    m = len(part)
+                    dst = FrameBatch.interleaved(dec.fmt, w, h, m, device=dev, storage=out.storage[:m])
+                    ops.stall_compose(sb, [pos[s] if s >= 0 else -1 for s, _ in part], [sp for _, sp in part],
+                                      dst=dst)
+                    data, sizes = enc.encode_host(dst)
+                    o = 0
+                    for k in sizes.tolist():
+                        packets.append(data[o:o + k].tobytes())
+                        o += k
+                ok = True
+            finally:
+                release_encoder(enc, ok=ok)
+        wr = avi.AviWriter(dst_path, w, h, rate, extradata=info["extradata"],
+                           info={b"ISFT": provenance(dec.slices).encode()})
+        try:
+            j = 0
+            for s, sp in seq:
+                if sp >= 0 or s < 0:
+                    wr.write_packet(packets[j])
+                    j += 1
+                else:
+                    wr.write_packet(packet(s))
+        except BaseException:
+            wr.abort()
+            raise
         wr.close()
     return len(seq)

@@ -16,6 +16,7 @@ from .frames import FrameBatch
 
 FLAGS = {"bilinear": 0x2, "bicubic": 0x4, "lanczos": 0x200}
 PARAM_DEFAULT = 123456.0
+PLAN_GENERIC = 0x10000000  # PP_PLAN_GENERIC (ABI v5)
 
 _contexts = {}
 
@@ -63,14 +64,18 @@ class Scaler:
     """
 
     def __init__(self, src_fmt, sw, sh, dst_fmt, dw, dh, flags="bicubic", param0=None, param1=None,
-                 device=None, chain=False):
+                 device=None, chain=False, generic=False):
         """chain=True: create_avpvs_segment's two stages (scale into the overlay's
         yuv420p, then yuv420p -> dst_fmt bicubic at the same size) as one plan
-        (pp_scale_chain_plan_create): one launch when kernel_path > 0."""
+        (pp_scale_chain_plan_create): one launch when kernel_path > 0.
+        generic=True: the general scale_kernel even where the strip kernel
+        applies (PP_PLAN_GENERIC; both are bit-exact, tests run both)."""
         self.src_fmt, self.dst_fmt = formats.fmt(src_fmt), formats.fmt(dst_fmt)
         self.sw, self.sh, self.dw, self.dh = int(sw), int(sh), int(dw), int(dh)
         self.ctx = context(device)
         fl = FLAGS[flags] if isinstance(flags, str) else int(flags)
+        if generic:
+            fl |= PLAN_GENERIC
         h = ctypes.c_void_p()
         create = lib().pp_scale_chain_plan_create if chain else lib().pp_scale_plan_create
         check(create(

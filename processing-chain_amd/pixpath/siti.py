@@ -319,13 +319,25 @@ def siti_from_yaml(src_file, with_depth=False):
     return float(e["si"]), float(e["ti"])
 
 
-def complexity_parse_args(argv=None):
-    """util/complexity_classification.py:91-131, plus --siti {yaml,gpu,none}."""
+def _script_dir():
+    """The directory of the running script (the reference's
+    util/complexity_classification.py when it calls complexity_main, as
+    INTEGRATION.md section 4 wires it), else the working directory."""
+    import sys
+    f = getattr(sys.modules.get("__main__"), "__file__", None)
+    return os.path.dirname(os.path.abspath(f)) if f else os.getcwd()
+
+
+def complexity_parse_args(argv=None, script_dir=None):
+    """util/complexity_classification.py:91-131, plus --siti {yaml,gpu,none}.
+    --tmp-dir defaults to `complexityAnalysis` next to the script, as the
+    reference's (:100-105: os.path.dirname(os.path.abspath(__file__)));
+    script_dir overrides which script that is."""
     import argparse
     ap = argparse.ArgumentParser(description="Complexity classification",
                                  formatter_class=argparse.ArgumentDefaultsHelpFormatter)
     ap.add_argument("-i", "--input", required=True, nargs="+", help="Input files (SRCs)")
-    ap.add_argument("-t", "--tmp-dir", default=os.path.join(os.getcwd(), "complexityAnalysis"),
+    ap.add_argument("-t", "--tmp-dir", default=os.path.join(script_dir or _script_dir(), "complexityAnalysis"),
                     help="Path to (temporary) complexity analysis folder")
     ap.add_argument("-p", "--parallelism", default=1, help="Number of parallel encodes")
     ap.add_argument("-o", "--output-file", default="complexity_classification.csv", help="Filename of CSV output file")
@@ -340,7 +352,7 @@ def complexity_parse_args(argv=None):
     return ap.parse_args(argv)
 
 
-def complexity_main(argv=None):
+def complexity_main(argv=None, script_dir=None):
     """util/complexity_classification.py:144-247 with `si`, `ti` columns appended
     (SI/TI of each SRC: its <src>.yaml from analyse_src, else -- with --siti gpu --
     measured on the MI355X).  Without them the CSV is byte-identical to the
@@ -352,7 +364,7 @@ def complexity_main(argv=None):
 
     import pandas as pd
     log = logging.getLogger("main")
-    a = complexity_parse_args(argv)
+    a = complexity_parse_args(argv, script_dir)
     if a.verbose:
         log.setLevel(logging.DEBUG)
     if not os.path.isdir(a.tmp_dir):

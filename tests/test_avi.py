@@ -76,3 +76,44 @@ def test_two_stream_avi_takes_the_video_stream(tmp_path, video_first):
                                                                                         extra)
     info2, index = avi.scan(path)
     assert [s for _, s in index] == [len(p) for p in vpk]
+
+
+def test_info_tag_and_atomic_output(tmp_path):
+    """The encoder provenance (RIFF INFO ISFT) round trips; the file appears
+    under its name only on close(), and abort() leaves nothing behind (the
+    builders' skip-if-exists rule never sees a partial AVPVS)."""
+    import os
+    path = str(tmp_path / "p.avi")
+    w = avi.AviWriter(path, 64, 32, 60, extradata=b"x", info={b"ISFT": b"pixpath ffv1-gpu v3 intra 8x8 slices"})
+    w.write_packet(b"abc")
+    assert not os.path.exists(path) and os.path.exists(path + ".part")
+    w.close()
+    info, pk = avi.read_packets(path)
+    assert pk == [b"abc"] and info["tags"][b"ISFT"] == b"pixpath ffv1-gpu v3 intra 8x8 slices"
+    assert not os.path.exists(path + ".part")
+    bad = str(tmp_path / "bad.avi")
+    w = avi.AviWriter(bad, 64, 32, 60)
+    w.write_packet(b"abc")
+    w.abort()
+    assert not os.path.exists(bad) and not os.path.exists(bad + ".part")
+
+
+@pytest.mark.parametrize("limit", [avi.RIFF_LIMIT, 20000])
+def test_batched_writes_equal_per_packet_writes(tmp_path, limit):
+    """write_packets (one writev per up to ~330 packets) lays out exactly the
+    file write_packet does, RIFF splits included."""
+    rng = np.random.default_rng(3)
+    sizes = [int(rng.integers(1, 3000)) for _ in range(700)]
+    data = rng.integers(0, 256, sum(sizes), dtype=np.uint8)
+    a, b = str(tmp_path / "a.avi"), str(tmp_path / "b.avi")
+    w = avi.AviWriter(a, 64, 32, 60, extradata=b"e", riff_limit=limit)
+    off = 0
+    for n in sizes:
+        w.write_packet(data[off:off + n])
+        off += n
+    w.close()
+    w = avi.AviWriter(b, 64, 32, 60, extradata=b"e", riff_limit=limit)
+    w.write_packets(data[:sizes[0] + sizes[1]], sizes[:2])
+    w.write_packets(data[sizes[0] + sizes[1]:], sizes[2:])
+    w.close()
+    assert open(a, "rb").read() == open(b, "rb").read()

@@ -101,8 +101,12 @@ def test_gpu_ffv1_opt_in_flags(monkeypatch):
     """PIXPATH_FFV1=gpu: AVPVS writers encode FFV1 on the GPU, AVPVS readers decode it there."""
     from pixpath import ffmpeg as pff
     monkeypatch.setenv("PIXPATH_FFV1", "gpu")
+    monkeypatch.delenv("PIXPATH_FFV1_SLICES", raising=False)
     a = pff._gpu_cli("avpvs", ["-y", "--vopts", pff.FFV1_OPTS, "/o.avi"])
-    assert a.endswith("--gpu-ffv1 /o.avi")
+    assert a.endswith("--gpu-ffv1 --ffv1-slices 8x8 /o.avi")
+    monkeypatch.setenv("PIXPATH_FFV1_SLICES", "16x16")
+    assert pff._gpu_cli("avpvs", ["-y", "--vopts", pff.FFV1_OPTS, "/o.avi"]).endswith("--ffv1-slices 16x16 /o.avi")
+    monkeypatch.delenv("PIXPATH_FFV1_SLICES")
     assert pff._gpu_cli("avpvs", ["-y", "--vopts", "-c:v libx264", "/o.mp4"]).endswith("--ffv1-input /o.mp4")
     assert pff._gpu_cli("cpvs", ["-y", "/c.avi"]).endswith("--gpu-ffv1 /c.avi")
     assert pff._gpu_cli("stall", ["-y", "/s.avi"]).endswith("--gpu-ffv1 /s.avi")
@@ -205,3 +209,46 @@ def test_ffv1_writer_slice_grid_setting(monkeypatch):
         monkeypatch.setenv("PIXPATH_FFV1_SLICES", bad)
         with pytest.raises(ValueError):
             ffv1.default_slices()
+
+
+def test_pixpath_ffv1_detection_and_reader_fallback(tmp_path, monkeypatch):
+    """Only AVIs whose FFV1 configuration record is exactly pixpath's encoder's
+    (for their format, size and slice grid) go to the GPU decoder; anything
+    else (FFmpeg's `-coder 1 -context 1` record, a corrupt record, another
+    codec) falls back to ffmpeg's decoder through pixpath.io."""
+    from pixpath import avi, ffv1, io as pio
+    rec = ffv1.Ffv1Encoder("yuv422p10le", 640, 360, slices=(4, 4), host_only=True).extradata
+    base = {"fourcc": b"FFV1", "w": 640, "h": 360}
+    assert ffv1.is_pixpath_ffv1(dict(base, extradata=rec))
+    assert not ffv1.is_pixpath_ffv1(dict(base, extradata=rec[:-1] + bytes([rec[-1] ^ 1])))  # CRC
+    assert not ffv1.is_pixpath_ffv1(dict(base, extradata=b"\x00" * 40))
+    assert not ffv1.is_pixpath_ffv1(dict(base, fourcc=b"H264", extradata=rec))
+    other = ffv1.Ffv1Encoder("yuv422p10le", 640, 360, slices=(2, 2), host_only=True).extradata
+    assert ffv1.is_pixpath_ffv1(dict(base, extradata=other))  # its own grid: still pixpath's
+    path = str(tmp_path / "ffmpeg_ffv1.avi")
+    w = avi.AviWriter(path, 640, 360, 60, extradata=b"not-pixpath-record")
+    w.write_packet(b"\x00" * 16)
+    w.close()
+    sentinel = object()
+    monkeypatch.setattr(pio, "open_reader", lambda p, **k: sentinel)
+    assert ffv1.open_avpvs_reader(path) is sentinel
+    assert ffv1.open_avpvs_reader(str(tmp_path / "x.y4m")) is sentinel
+
+
+def test_codec_provenance_in_the_p03_log_line(monkeypatch):
+    """p03 logs every builder string as an `ffmpegCommand:` line
+    (p03_generateAvPvs.py:41-59).  With the GPU FFV1 (default) the line names
+    the codec and slice grid; with PIXPATH_FFV1=ffmpeg it carries the
+    reference's own FFV1 options (the reference-faithful bitstream)."""
+    from pixpath import ffmpeg as pff
+    from pixpath.provenance import p03_log_line
+    args = ["-y", "--input", "/db/videoSegments/seg.mkv", "--size", "1920x1080", "--pix-fmt", "yuv422p10le",
+            "--vopts", pff.FFV1_OPTS, "--aopts", "-c:a flac", "/db/avpvs/P.avi"]
+    monkeypatch.delenv("PIXPATH_FFV1", raising=False)
+    monkeypatch.setenv("PIXPATH_FFV1_SLICES", "16x16")
+    line = p03_log_line(pff._collapse(pff._gpu_cli("avpvs", args)), "/db/videoSegments", "/db/srcVid")
+    assert line.startswith("ffmpegCommand: ") and "--gpu-ffv1 --ffv1-slices 16x16" in line
+    assert "seg.mkv" in line and "/db/videoSegments/" not in line
+    monkeypatch.setenv("PIXPATH_FFV1", "ffmpeg")
+    line = p03_log_line(pff._collapse(pff._gpu_cli("avpvs", args)), "/db/videoSegments", "/db/srcVid")
+    assert "--gpu-ffv1" not in line and "-coder 1 -context 1 -slicecrc 1" in line

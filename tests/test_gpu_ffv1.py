@@ -357,3 +357,63 @@ def test_writer_pool_reuses_encoder_across_pvses(gpu, tmp_path):
             for p in range(3):
                 np.testing.assert_array_equal(dec[p], f[p], err_msg="PVS %d frame %d plane %d" % (k, i, p))
     assert encs[1] is encs[0]
+
+
+def test_record_budget_split_keeps_the_bytes(gpu):
+    """The per-slice renorm-record budget (pp_ffv1_encode_packets): a batch of
+    mostly smooth frames with noise frames among them overflows the budget
+    of a full launch, is re-coded in halves down to launches where every
+    slice fits, and its packets are byte-identical to frame-by-frame encodes
+    (max_frames=1: always the worst-case records) and to the C restatement."""
+    from pixpath import ffv1
+    w, h, grid = 640, 360, (4, 4)
+    rng = np.random.default_rng(91)
+    frames = [synth.smooth_frame(i, po.YUV422P10LE, w, h) for i in range(8)]
+    frames[5] = synth.noise_frame(rng, po.YUV422P10LE, w, h)
+    enc = ffv1.Ffv1Encoder("yuv422p10le", w, h, slices=grid, max_frames=8, device=gpu)
+    pkts = enc.encode_to_host(_batch(gpu, "yuv422p10le", frames))
+    assert enc.launches > 1
+    one = ffv1.Ffv1Encoder("yuv422p10le", w, h, slices=grid, max_frames=1, device=gpu)
+    for f, planes in enumerate(frames):
+        assert pkts[f] == one.encode_to_host(_batch(gpu, "yuv422p10le", [planes]))[0], "frame %d" % f
+    assert one.launches == 1
+    for f in (4, 5):
+        assert pkts[f] == ref.encode_frame(frames[f], 10, 1, 0, *grid)
+    smooth = ffv1.Ffv1Encoder("yuv422p10le", w, h, slices=grid, max_frames=8, device=gpu)
+    smooth.encode_to_host(_batch(gpu, "yuv422p10le", frames[:5]))
+    assert smooth.launches == 1
+
+
+def test_encoder_footprint(gpu):
+    """A 600-frame 1080p yuv422p10le encoder (the AVPVS writer's) holds less
+    than 18 GB of HBM: tokens 10 GB, renorm records ~5 GB, context states
+    1.6 GB; the slice bytes are resolved in place over the records."""
+    from pixpath import ffv1
+    enc = ffv1.Ffv1Encoder("yuv422p10le", 1920, 1080, slices=(8, 8), max_frames=600, device=gpu)
+    assert enc.memory_bytes < 18e9
+
+
+def test_failed_writer_leaves_no_file_and_frees_its_encoder(gpu, tmp_path, monkeypatch):
+    """An encode that fails inside the AVI writer: close() raises, neither the
+    output nor its .part file remains, and the encoder is not pooled."""
+    import os
+    import torch
+    from pixpath import ffv1
+    from pixpath.frames import FrameBatch
+    ffv1.clear_pool()
+    path = str(tmp_path / "PVS.avi")
+    wr = ffv1.Ffv1AviWriter(path, "yuv422p10le", 320, 180, 60, slices=(4, 4), batch=8, device=gpu)
+    enc = wr.enc
+
+    def boom(*a, **k):
+        raise RuntimeError("injected encode failure")
+    monkeypatch.setattr(enc, "encode_host", boom)
+    src = FrameBatch.interleaved("yuv422p10le", 320, 180, 3, device=gpu)
+    src.storage.zero_()
+    wr.write_device(src)
+    with pytest.raises(RuntimeError, match="injected"):
+        wr.close()
+    assert not os.path.exists(path) and not os.path.exists(path + ".part")
+    again = ffv1.acquire_encoder("yuv422p10le", 320, 180, slices=(4, 4), max_frames=8, device=gpu)
+    assert again is not enc
+    torch.cuda.synchronize()

@@ -55,16 +55,14 @@ def _frames(content, fmt, w, h, n, seed):
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "%dx%d_f%d->%dx%d_f%d_%x" % (c[1], c[2], c[0], c[4], c[5], c[3], c[6]))
 def test_scale_matches_oracle(gpu, case, kernel, monkeypatch):
     """Both scaler kernels (strip kernel where the plan allows it, and the
-    general kernel forced by PIXPATH_SCALE_KERNEL=generic) against the oracle."""
+    general kernel forced by the PP_PLAN_GENERIC plan flag) against the oracle."""
     from pixpath import ops
     from pixpath.frames import FrameBatch
     sf, sw, sh, df, dw, dh, flags, content = case
-    if kernel == "generic":
-        monkeypatch.setenv("PIXPATH_SCALE_KERNEL", "generic")
     n = 2
     frames = _frames(content, sf, sw, sh, n, seed=910)
     src = FrameBatch.from_numpy(sf, synth.batch(frames), device=gpu)
-    sc = ops.Scaler(sf, sw, sh, df, dw, dh, flags=flags)
+    sc = ops.Scaler(sf, sw, sh, df, dw, dh, flags=flags, generic=kernel == "generic")
     if kernel == "generic":
         assert sc.kernel_path == 0
     out = sc(src).to_numpy()

@@ -79,14 +79,12 @@ def test_full_range_extremes(gpu, plan, kind, kernel, monkeypatch):
     from pixpath import ops
     from pixpath.frames import FrameBatch
     sf, sw, sh, df, dw, dh, flags = plan
-    if kernel == "generic":
-        monkeypatch.setenv("PIXPATH_SCALE_KERNEL", "generic")
     # output strip seams (256 columns) and segment seams (540 rows) mapped to source coordinates
     seams_x = [x * sw // dw for x in range(256, dw, 256)] + [x * sw // dw + 1 for x in range(256, dw, 256)]
     seams_y = [y * sh // dh for y in range(270, dh, 270)]
     frames = [synth.extreme_frame(kind, sf, sw, sh, seed=i, seams_x=seams_x, seams_y=seams_y) for i in range(2)]
     src = FrameBatch.from_numpy(sf, synth.batch(frames), device=gpu)
-    out = ops.Scaler(sf, sw, sh, df, dw, dh, flags=FLAGS[flags])(src).to_numpy()
+    out = ops.Scaler(sf, sw, sh, df, dw, dh, flags=FLAGS[flags], generic=kernel == "generic")(src).to_numpy()
     torch.cuda.synchronize()
     mx = (1 << po.fmt_info(df)[0]) - 1 if df not in (po.UYVY422, po.V210) else 255
     hit_clip = False

@@ -149,3 +149,14 @@ def test_complexity_dry_run_lists_encodes(fake_root, caplog):
         siti.complexity_main(["-i", os.path.join(fake_root, "SRC101.avi"), "-t", os.path.join(fake_root, "fresh"),
                               "-n"])
     assert e.value.code == 0
+
+
+def test_complexity_tmp_dir_default_is_next_to_the_script(tmp_path):
+    """--tmp-dir defaults to complexityAnalysis beside the calling script, as
+    the reference's (util/complexity_classification.py:100-105)."""
+    import os
+    from pixpath import siti
+    a = siti.complexity_parse_args(["-i", "x.avi"], script_dir="/opt/pc/util")
+    assert a.tmp_dir == os.path.join("/opt/pc/util", "complexityAnalysis")
+    b = siti.complexity_parse_args(["-i", "x.avi", "-t", str(tmp_path)])
+    assert b.tmp_dir == str(tmp_path)
