@@ -399,7 +399,13 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None):
     stage = Stage(sfmt, sw, sh, dfmt, dw, dh, lambda s, d, st: sc(s, d, stream=st))
     pl = Pipeline(stage, batch=60, device=dev.index)
     d = tempfile.mkdtemp(prefix="pixpath_e2e_")
-    paths = [os.path.join(d, "PVS%d.avi" % k) for k in range(n_pvs)]
+    # fresh output names per run: replacing a 1.2 GB AVI left by an earlier run
+    # frees its pages inside close() (0.2 s), which is not this run's work
+    runs = [0]
+
+    def new_paths(count):
+        runs[0] += 1
+        return [os.path.join(d, "r%d_PVS%d.avi" % (runs[0], k)) for k in range(count)]
     depth = depth or n_pvs  # every PVS of the run can be in flight at once
     t_res = time.perf_counter()
     made = ffv1.reserve_encoders(dfmt, dw, dh, depth, slices=(8, 8), max_frames=n_frames, device=dev.index)
@@ -407,6 +413,9 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None):
     reserve_s = time.perf_counter() - t_res
 
     def run(count):
+        for f in os.listdir(d):  # the previous run's files, outside the timed region
+            os.remove(os.path.join(d, f))
+        paths = new_paths(count)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         closers, errs, stats, n = [], [], [], 0
@@ -450,18 +459,17 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None):
         # the main thread's stages plus the wait for the last writers: the wall time
         st["explained_s"] = round(sum(setup_s) + sum(pipe_s) + st["tail_s"], 4)
         st["explained_frac"] = round(st["explained_s"] / dt, 4)
+        st["avi_bytes"] = os.path.getsize(paths[0])
         return n, dt, st
 
     try:
         run(1)  # warm-up (kernel loads, pinned buffers, the pipeline's device batches)
         n1, dt1, w1 = run(1)
-        size = os.path.getsize(paths[0])
+        size = w1["avi_bytes"]
         n, dt, ws = run(n_pvs)
     finally:
-        for p_ in paths:
-            for q_ in (p_, p_ + ".part"):
-                if os.path.exists(q_):
-                    os.remove(q_)
+        for f in os.listdir(d):
+            os.remove(os.path.join(d, f))
         os.rmdir(d)
     enc_mem = None
     try:

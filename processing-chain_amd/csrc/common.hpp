@@ -2,7 +2,9 @@
 // table, the context object.  See include/pixpath.h for the ABI.
 #pragma once
 
+#ifndef PIXPATH_HOST_ONLY  // `make sanitize`: the host parsers alone, built by g++ under ASan/UBSan
 #include <hip/hip_runtime.h>
+#endif
 
 #include <cstdarg>
 #include <cstdint>
@@ -36,12 +38,14 @@ void set_error(const char *fmt, ...);
         return (code);                     \
     } while (0)
 
+#ifndef PIXPATH_HOST_ONLY
 #define PP_HIP(expr)                                                              \
     do {                                                                          \
         hipError_t e_ = (expr);                                                   \
         if (e_ != hipSuccess)                                                     \
             PP_FAIL(PP_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));  \
     } while (0)
+#endif
 
 // Planar layout of a format: bit depth, chroma subsampling, plane count.
 struct FmtInfo {
@@ -90,7 +94,10 @@ inline int ffv1_lanes_per_wave(int dflt) {
 // frame, bands of one frame range) share an L2 and their halos are fetched
 // from HBM once.  A bijection on [0, n) for any n.
 constexpr int kXcds = 8;
-__host__ __device__ inline int xcd_remap(int b, int n) {
+#ifndef PIXPATH_HOST_ONLY
+__host__ __device__
+#endif
+inline int xcd_remap(int b, int n) {
     const int per = n / kXcds, rem = n % kXcds;
     const int k = b % kXcds, q = b / kXcds;
     return k < rem ? k * (per + 1) + q : rem * (per + 1) + (k - rem) * per + q;
