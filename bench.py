@@ -116,6 +116,8 @@ def parse():
     ap.add_argument("--allow-tuning", action="store_true",
                     help="run with PIXPATH_* measurement overrides set (tools/ only; recorded in the line)")
     ap.add_argument("--e2e-pvs", type=int, default=4, help="PVSes in a row for the e2e_avpvs line")
+    ap.add_argument("--e2e-encode", default="shared", choices=["shared", "private"],
+                    help="e2e_avpvs writers: one encode stream + lock per device (product), or own streams")
     ap.add_argument("--cpu-e2e-seconds", type=float, default=4.0, help="CPU counterpart of e2e_avpvs: sample length")
     return ap.parse_args()
 
@@ -349,7 +351,7 @@ def pcie_pipeline(wl, n_frames, dev, batch=60):
                     "host fill of the pinned input is included, decode/encode are not"}
 
 
-def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None):
+def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None, shared=True):
     """The product path of `cli avpvs --gpu-ffv1` end to end (SURVEY.md 8d's
     third row): dense host frames -> pinned batches -> H2D -> strip_kernel ->
     FFV1 encode of the DEVICE output (no D2H of pixels) -> packets D2H -> AVI
@@ -429,7 +431,8 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None):
                 errs.append(e)
         for k in range(count):
             tw = time.perf_counter()
-            wr = Ffv1AviWriter(paths[k], dfmt, dw, dh, 60, slices=(8, 8), batch=n_frames, device=dev.index)
+            wr = Ffv1AviWriter(paths[k], dfmt, dw, dh, 60, slices=(8, 8), batch=n_frames, device=dev.index,
+                               shared=shared)
             tp = time.perf_counter()
             n += pl.run(MemReader(), wr)
             te = time.perf_counter()
@@ -481,6 +484,7 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None):
     ffv1.clear_pool()
     return {"frames_per_s": round(n / dt, 1), "frames": n, "pvs": n_pvs, "seconds": round(dt, 3), "stages": ws,
             "single_pvs": {"frames_per_s": round(n1 / dt1, 1), "seconds": round(dt1, 3), "stages": w1},
+            "writers": "one encode stream and lock per device" if shared else "own streams, concurrent encodes",
             "encoder_pool": {"depth": depth, "created": made, "reserve_s": round(reserve_s, 3),
                              "bytes_per_writer": enc_mem},
             "avi_bytes_per_pvs": size, "compression": round(n1 * frame_bytes(dfmt, dw, dh) / size, 3),
@@ -671,7 +675,7 @@ def main():
     if world == 1 and siti_wh and not args.no_siti_file:
         out["siti_file"] = siti_file(dev)
     if world == 1 and args.workload == "config2" and not args.no_e2e:
-        out["e2e_avpvs"] = e2e_avpvs(wl, 600, dev, n_pvs=args.e2e_pvs)
+        out["e2e_avpvs"] = e2e_avpvs(wl, 600, dev, n_pvs=args.e2e_pvs, shared=args.e2e_encode == "shared")
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, wl)
         ce = out["cpu_baseline"].get("e2e") if out["cpu_baseline"] else None

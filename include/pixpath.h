@@ -276,6 +276,9 @@ int64_t pp_ffv1_encode(pp_ffv1_enc *enc, const pp_frames *src, int nframes, uint
 int64_t pp_ffv1_encode_packets(pp_ffv1_enc *enc, const pp_frames *src, int nframes, int64_t *frame_sizes,
                                const uint8_t **packets, void *stream);
 int pp_ffv1_encode_stats(const pp_ffv1_enc *enc, int *launches);
+/* Grow the encoder's packet buffer to `packet_bytes` now (a writer process
+ * sizes it once, before its first PVS, instead of inside the first encode). */
+int pp_ffv1_encoder_reserve(pp_ffv1_enc *enc, int64_t packet_bytes);
 int pp_ffv1_encoder_memory(const pp_ffv1_enc *enc, int64_t *bytes);
 /* FFV1 decoder (the CPVS stage reads the AVPVS back, lib/ffmpeg.py:1149):
  * version 3 intra streams with the range coder's default state table, one

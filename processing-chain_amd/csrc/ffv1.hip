@@ -887,6 +887,13 @@ extern "C" int64_t pp_ffv1_encode_packets(pp_ffv1_enc *E, const pp_frames *src, 
     return total;
 }
 
+extern "C" int pp_ffv1_encoder_reserve(pp_ffv1_enc *E, int64_t packet_bytes) {
+    if (!E || packet_bytes < 0) PP_FAIL(PP_ERR_INVALID, "bad argument");
+    if (!E->ctx) PP_FAIL(PP_ERR_INVALID, "host-only encoder");
+    PP_HIP(hipSetDevice(E->ctx->device));
+    return pk_reserve(E, packet_bytes, 0, nullptr);
+}
+
 extern "C" int pp_ffv1_encode_stats(const pp_ffv1_enc *E, int *launches) {
     if (!E || !launches) PP_FAIL(PP_ERR_INVALID, "null argument");
     *launches = E->launches;

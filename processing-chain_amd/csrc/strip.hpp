@@ -241,8 +241,20 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
     commit(pf, next_src, chunk_hi[y_begin / cho]);
     const bool lane_any = cx < nx, lane_full = cx + 4 <= nx;
     const int xo = x0 + cx;
+    // clamped V pass (wave-uniform): when the strip ends on a 4-column group
+    // and rows take vector stores, a lane past the strip's last group reads
+    // that group's window columns and stores its outputs again -- the same
+    // bytes to the same address -- so the V-pass row loop has no per-lane
+    // branch (a divergent `continue` per stored row turned every unrolled row
+    // group into exec-mask bookkeeping: more SALU than VALU instructions in
+    // the chain kernel, profiles/r3/chain_ablation.txt)
+    const bool clamp = (nx & 3) == 0 && a.vec_dst;
+    const int cxv = clamp ? min(cx, nx - 4) : cx;
+    const int xov = x0 + cxv;
     const int64_t dls = a.dls[p];
     const int vtp = J.vtp;
+    const int jdw = J.dw;
+    const int jfuse = FUSE >= 8 ? J.fuse : 0;
     const kconst int32_t *vrow = as_kconst<int32_t>(J.vrow16);
     for (int y0 = y_begin; y0 < y_end; y0 += cho) {
         const int ci = y0 / cho;
@@ -319,8 +331,10 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
         const int ny = min(cho, y_end - y0);
         // VT (= vtp) tap pairs, compile-time per instance: every window read of
         // a row is in flight before the first v_dot2 waits on one
-        auto vpass = [&](auto vt_c) {
+        auto vpass = [&](auto vt_c, auto cl_c) {
             constexpr int VT = decltype(vt_c)::value;
+            constexpr bool CL = decltype(cl_c)::value;  // clamped lanes: no per-lane branch
+            const int vx = CL ? cxv : cx, vxo = CL ? xov : xo;
             // row records (window base row + VT tap pairs) of G rows at a time
             // through the scalar cache: one exposed scalar-load latency per
             // group, not per row (the ds_reads of a row depend on its base)
@@ -342,7 +356,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                     if (yy >= ny) break;
                     const int y = y0 + yy;
                     uint8_t *drow_p = dbase + (int64_t)y * dls;
-                    const uint4 *rp = reinterpret_cast<const uint4 *>(win + ((vb[i] - nbase) >> 1) * TW + cx);
+                    const uint4 *rp = reinterpret_cast<const uint4 *>(win + ((vb[i] - nbase) >> 1) * TW + vx);
                     uint4 q[VT];
 #pragma unroll
                     for (int j = 0; j < VT; ++j) q[j] = rp[j * (TW / 4)];
@@ -353,7 +367,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                         uint32_t d4 = 0x40404040u;
                         if (a.dither) {
                             const uint64_t rv = as_kconst<uint64_t>(c_dither64)[y & 7];
-                            const int rot = ((xo + J.dither_off) & 7) * 8;
+                            const int rot = ((vxo + J.dither_off) & 7) * 8;
                             d4 = (uint32_t)(rot ? (rv >> rot) | (rv << (64 - rot)) : rv);
                         }
 #pragma unroll
@@ -370,27 +384,27 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                         acc[2] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].z), c2, acc[2], false);
                         acc[3] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].w), c2, acc[3], false);
                     }
-                    if (!lane_any || (PP_ABLATE(a.debug) & 1)) continue;
+                    if ((!CL && !lane_any) || (PP_ABLATE(a.debug) & 1)) continue;
                     constexpr int sh = OUTB == 8 ? 19 : 11 + 16 - OUTB;
                     constexpr int mx = (1 << OUTB) - 1;
                     int o[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) o[j] = min(max(acc[j] >> sh, 0), mx);
                     if constexpr (FUSE >= 8) {
-                        if (J.fuse == 2) {  // into ring2 (second-stage input), 15-bit
-                            uint16_t *r16 = reinterpret_cast<uint16_t *>(ring2 + ((y - base2) >> 1) * TW + cx);
+                        if (jfuse == 2) {  // into ring2 (second-stage input), 15-bit
+                            uint16_t *r16 = reinterpret_cast<uint16_t *>(ring2 + ((y - base2) >> 1) * TW + vx);
 #pragma unroll
                             for (int j = 0; j < 4; ++j) r16[2 * j + (y & 1)] = static_cast<uint16_t>(o[j] << 7);
                             __builtin_amdgcn_sched_barrier(0);
                             continue;
                         }
-                        if (J.fuse == 1) {  // identity second stage: one 4096 tap on x << 7
+                        if (jfuse == 1) {  // identity second stage: one 4096 tap on x << 7
                             constexpr int r2 = FUSE == 8 ? 64 << 12 : 1 << (10 + 16 - FUSE);
                             constexpr int s2 = FUSE == 8 ? 19 : 11 + 16 - FUSE;
                             int w[4];
 #pragma unroll
                             for (int j = 0; j < 4; ++j) w[j] = ((o[j] << 19) + r2) >> s2;
-                            store4<FUSE>(drow_p, xo, w, lane_full && a.vec_dst, J.dw);
+                            store4<FUSE>(drow_p, vxo, w, CL || (lane_full && a.vec_dst), jdw);
                             __builtin_amdgcn_sched_barrier(0);
                             continue;
                         }
@@ -400,27 +414,8 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
                             if (xo + j < J.dw) pk[(xo + j) * J.pk_step] = (uint8_t)o[j];
-                    } else if constexpr (OUTB == 8) {
-                        if (lane_full && a.vec_dst) {
-                            *reinterpret_cast<uint32_t *>(drow_p + xo) =
-                                (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | ((uint32_t)o[3] << 24);
-                        } else {
-#pragma unroll
-                            for (int j = 0; j < 4; ++j)
-                                if (xo + j < J.dw) drow_p[xo + j] = (uint8_t)o[j];
-                        }
                     } else {
-                        uint16_t *d16 = reinterpret_cast<uint16_t *>(drow_p);
-                        if (lane_full && a.vec_dst) {
-                            uint2 v;
-                            v.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-                            v.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-                            *reinterpret_cast<uint2 *>(d16 + xo) = v;
-                        } else {
-#pragma unroll
-                            for (int j = 0; j < 4; ++j)
-                                if (xo + j < J.dw) d16[xo + j] = (uint16_t)o[j];
-                        }
+                        store4<OUTB>(drow_p, vxo, o, CL || (lane_full && a.vec_dst), jdw);
                     }
                     // keep the next row's window reads behind this row's math
                     // (hoisting them all costs ~50 VGPRs and two waves/SIMD)
@@ -428,27 +423,33 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                 }
             }
         };
-        switch (vtp) {  // uniform, once per chunk; arms up to VTM only (register budget)
-        case 1: vpass(std::integral_constant<int, 1>{}); break;
-        case 2: if constexpr (VTM >= 2) vpass(std::integral_constant<int, 2>{}); break;
-        case 3: if constexpr (VTM >= 3) vpass(std::integral_constant<int, 3>{}); break;
-        case 4: if constexpr (VTM >= 4) vpass(std::integral_constant<int, 4>{}); break;
-        case 5: if constexpr (VTM >= 5) vpass(std::integral_constant<int, 5>{}); break;
-        case 6: if constexpr (VTM >= 6) vpass(std::integral_constant<int, 6>{}); break;
-        case 7: if constexpr (VTM >= 7) vpass(std::integral_constant<int, 7>{}); break;
-        default: if constexpr (VTM >= 8) vpass(std::integral_constant<int, 8>{}); break;
-        }
+        auto vdispatch = [&](auto cl_c) {
+            switch (vtp) {  // uniform, once per chunk; arms up to VTM only (register budget)
+            case 1: vpass(std::integral_constant<int, 1>{}, cl_c); break;
+            case 2: if constexpr (VTM >= 2) vpass(std::integral_constant<int, 2>{}, cl_c); break;
+            case 3: if constexpr (VTM >= 3) vpass(std::integral_constant<int, 3>{}, cl_c); break;
+            case 4: if constexpr (VTM >= 4) vpass(std::integral_constant<int, 4>{}, cl_c); break;
+            case 5: if constexpr (VTM >= 5) vpass(std::integral_constant<int, 5>{}, cl_c); break;
+            case 6: if constexpr (VTM >= 6) vpass(std::integral_constant<int, 6>{}, cl_c); break;
+            case 7: if constexpr (VTM >= 7) vpass(std::integral_constant<int, 7>{}, cl_c); break;
+            default: if constexpr (VTM >= 8) vpass(std::integral_constant<int, 8>{}, cl_c); break;
+            }
+        };
+        if (clamp && FUSE != 1) vdispatch(std::true_type{});
+        else vdispatch(std::false_type{});
         if constexpr (FUSE >= 8) {
             // ---- second stage (fuse 2): vertical filter of the ring2 rows ----
-            if (J.fuse == 2 && !(PP_ABLATE(a.debug) & 16)) {  // debug 16: no second stage (timing only)
+            if (jfuse == 2 && !(PP_ABLATE(a.debug) & 16)) {  // debug 16: no second stage (timing only)
                 __syncthreads();  // this chunk's first-stage rows are in ring2
                 const int lo2 = chunk2[4 * ci], hi2 = chunk2[4 * ci + 1];
                 const kconst int32_t *vrow2 = as_kconst<int32_t>(J.vrow2);
                 // VT2 tap pairs compile-time; the row records of G2 rows come
                 // through the scalar cache at once (as in the first stage's V
                 // pass: one exposed scalar-load latency per group, not per row)
-                auto pass2 = [&](auto vt_c) {
+                auto pass2 = [&](auto vt_c, auto cl_c) {
                     constexpr int VT2 = decltype(vt_c)::value;
+                    constexpr bool CL = decltype(cl_c)::value;
+                    const int vx = CL ? cxv : cx, vxo = CL ? xov : xo;
                     constexpr int G2 = 4;
                     for (int g0 = lo2 + rg; g0 < hi2; g0 += 4 * G2) {
                         int vb[G2];
@@ -464,7 +465,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                         for (int i = 0; i < G2; ++i) {
                             const int r2 = g0 + 4 * i;
                             if (r2 >= hi2) break;
-                            const uint4 *rp = reinterpret_cast<const uint4 *>(ring2 + ((vb[i] - base2) >> 1) * TW + cx);
+                            const uint4 *rp = reinterpret_cast<const uint4 *>(ring2 + ((vb[i] - base2) >> 1) * TW + vx);
                             uint4 q[VT2];
 #pragma unroll
                             for (int j = 0; j < VT2; ++j) q[j] = rp[j * (TW / 4)];
@@ -479,22 +480,26 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                                 acc[2] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].z), c2, acc[2], false);
                                 acc[3] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].w), c2, acc[3], false);
                             }
-                            if (!lane_any) continue;
+                            if (!CL && !lane_any) continue;
                             constexpr int s2 = FUSE == 8 ? 19 : 11 + 16 - FUSE;
                             int w[4];
 #pragma unroll
                             for (int j = 0; j < 4; ++j) w[j] = min(max(acc[j] >> s2, 0), (1 << FUSE) - 1);
-                            store4<FUSE>(dbase + (int64_t)r2 * dls, xo, w, lane_full && a.vec_dst, J.dw);
+                            store4<FUSE>(dbase + (int64_t)r2 * dls, vxo, w, CL || (lane_full && a.vec_dst), jdw);
                             __builtin_amdgcn_sched_barrier(0);
                         }
                     }
                 };
-                switch (J.vtp2) {  // uniform; the host allows <= 4 pairs
-                case 1: pass2(std::integral_constant<int, 1>{}); break;
-                case 2: pass2(std::integral_constant<int, 2>{}); break;
-                case 3: pass2(std::integral_constant<int, 3>{}); break;
-                default: pass2(std::integral_constant<int, 4>{}); break;
-                }
+                auto dispatch2 = [&](auto cl_c) {
+                    switch (J.vtp2) {  // uniform; the host allows <= 4 pairs
+                    case 1: pass2(std::integral_constant<int, 1>{}, cl_c); break;
+                    case 2: pass2(std::integral_constant<int, 2>{}, cl_c); break;
+                    case 3: pass2(std::integral_constant<int, 3>{}, cl_c); break;
+                    default: pass2(std::integral_constant<int, 4>{}, cl_c); break;
+                    }
+                };
+                if (clamp) dispatch2(std::true_type{});
+                else dispatch2(std::false_type{});
             }
         }
         __builtin_amdgcn_s_setprio(0);

@@ -23,7 +23,7 @@ EXPORTS = (
     "pp_stream_wait_event", "pp_event_synchronize", "pp_event_elapsed_ms", "pp_copy_async", "pp_copy2d_async",
     "pp_frames_copy_async", "pp_annexb_frame_sizes", "pp_ivf_frame_sizes",
     "pp_ffv1_encoder_create", "pp_ffv1_encoder_destroy", "pp_ffv1_extradata", "pp_ffv1_encode",
-    "pp_ffv1_encode_packets", "pp_ffv1_encode_stats", "pp_ffv1_encoder_memory",
+    "pp_ffv1_encode_packets", "pp_ffv1_encode_stats", "pp_ffv1_encoder_memory", "pp_ffv1_encoder_reserve",
     "pp_ffv1_decoder_create", "pp_ffv1_decoder_destroy", "pp_ffv1_decoder_format", "pp_ffv1_decoder_slices", "pp_ffv1_decode",
 )
 PP_COPY_H2D, PP_COPY_D2H, PP_COPY_D2D = 1, 2, 3
@@ -107,6 +107,7 @@ def lib():
         "pp_ffv1_encode_packets": (i64, [vp, fr, i32, vp, ctypes.POINTER(vp), vp]),
         "pp_ffv1_encode_stats": (i32, [vp, ctypes.POINTER(i32)]),
         "pp_ffv1_encoder_memory": (i32, [vp, ctypes.POINTER(i64)]),
+        "pp_ffv1_encoder_reserve": (i32, [vp, i64]),
         "pp_ffv1_decoder_create": (i32, [vp, vp, i32, i32, i32, i32, ctypes.POINTER(vp)]),
         "pp_ffv1_decoder_destroy": (i32, [vp]),
         "pp_ffv1_decoder_format": (i32, [vp]),

@@ -66,6 +66,14 @@ class Ffv1Encoder:
         check(lib().pp_ffv1_encode_stats(self.handle, ctypes.byref(v)))
         return v.value
 
+    def reserve(self, packet_bytes):
+        """Size the device packet buffer and the pinned host buffer of
+        encode_host for `packet_bytes` of packets now (pinning ~2 GB of host
+        memory takes ~0.2 s: a writer does it before its first PVS)."""
+        check(lib().pp_ffv1_encoder_reserve(self.handle, int(packet_bytes)))
+        if getattr(self, "_host", None) is None or self._host.numel() < packet_bytes:
+            self._host = torch.empty(max(int(packet_bytes), 1 << 20), dtype=torch.uint8).pin_memory()
+
     def encode_packets(self, src, stream=None):
         """Encode a FrameBatch into the encoder's own device packet buffer:
         (device pointer, total bytes, numpy int64 frame sizes).  The packets
@@ -173,12 +181,16 @@ def reserve_encoders(fmt, w, h, count, slices=(8, 8), max_frames=600, device=Non
         idle = _POOL.setdefault(key, [])
         idle.extend(made)
         encs = list(idle)
+    fb = formats.frame_bytes(formats.fmt(fmt), w, h)
     for enc in encs:
         st = getattr(enc, "stages", None) or []
         while len(st) < stages:
             st.append(FrameBatch.interleaved(enc.fmt, enc.w, enc.h, enc.max_frames,
                                              device=torch.device("cuda", enc.ctx.device)))
         enc.stages = st
+        # packets of a full batch at 2:1 (video content codes at 2-5:1); a
+        # batch that codes larger grows the buffers in its encode
+        enc.reserve(enc.max_frames * fb // 2)
     return len(made)
 
 
@@ -232,6 +244,25 @@ class Ffv1Decoder:
         return dst
 
 
+_DEV_LOCK = threading.Lock()
+_DEV_STATE = {}  # device index -> (encode lock, encode stream, host-upload stream)
+
+
+def _device_state(device):
+    """One encode lock and one pair of streams per device and process, shared
+    by every AVI writer: the writers' encodes run one at a time on one stream.
+    Concurrent encodes from writer threads measured slower than serial ones
+    beside a running scale pipeline (e2e_avpvs: 0.58 s per 600-frame encode
+    when two overlap vs 0.19 s alone), and every extra stream shares one of
+    the process's few hardware queues with the pipeline's."""
+    with _DEV_LOCK:
+        st = _DEV_STATE.get(device)
+        if st is None:
+            st = _DEV_STATE[device] = (threading.Lock(), torch.cuda.Stream(torch.device("cuda", device)),
+                                       torch.cuda.Stream(torch.device("cuda", device)))
+        return st
+
+
 def provenance(slices):
     """The encoder tag written into the AVPVS (RIFF INFO ISFT) and echoed in
     the GPU command string p03 logs as `ffmpegCommand:` (p03_generateAvPvs.py:41-59)."""
@@ -252,9 +283,12 @@ class Ffv1AviWriter:
     packets come back in one pinned D2H and go into the AVI.  The encoder and
     its staging batches come from the process's pool (acquire_encoder)."""
 
-    def __init__(self, path, fmt, w, h, rate, slices=None, batch=600, device=None):
+    def __init__(self, path, fmt, w, h, rate, slices=None, batch=600, device=None, shared=True):
         """slices: the FFV1 slice grid (default PIXPATH_FFV1_SLICES, else 8x8;
-        16x16 encodes ~1.3x faster at ~7 % larger files)."""
+        16x16 encodes ~1.3x faster at ~7 % larger files).
+        shared: encode on the device's shared stream under its encode lock
+        (_device_state); False gives the writer its own streams and lets its
+        encodes overlap other writers' (bench comparison only)."""
         import time
         from . import avi
         t0 = time.perf_counter()
@@ -274,8 +308,12 @@ class Ffv1AviWriter:
             e.set()
         self.cur, self.fill = 0, 0
         self.free[0].clear()
-        self.stream = torch.cuda.Stream(self.device)
-        self.put_stream = torch.cuda.Stream(self.device)  # host-frame uploads
+        if shared:
+            self.lock, self.stream, self.put_stream = _device_state(self.device.index)
+        else:
+            self.lock = threading.Lock()
+            self.stream = torch.cuda.Stream(self.device)
+            self.put_stream = torch.cuda.Stream(self.device)  # host-frame uploads
         self.avi = avi.AviWriter(path, w, h, rate, extradata=self.enc.extradata,
                                  info={b"ISFT": provenance(self.enc.slices).encode()})
         self.frames = 0
@@ -310,10 +348,11 @@ class Ffv1AviWriter:
                     ev.synchronize()  # the frames of this batch are in the staging batch
                     src = FrameBatch.interleaved(self.fmt, self.w, self.h, n, device=self.device,
                                                  storage=self.enc.stages[slot].storage[:n])
-                    t0 = time.perf_counter()
-                    with torch.cuda.stream(self.stream):
-                        data, sizes = self.enc.encode_host(src, stream=self.stream)
-                    t1 = time.perf_counter()
+                    with self.lock:
+                        t0 = time.perf_counter()
+                        with torch.cuda.stream(self.stream):
+                            data, sizes = self.enc.encode_host(src, stream=self.stream)
+                        t1 = time.perf_counter()
                     self.avi.write_packets(data, sizes)
                     t2 = time.perf_counter()
                     self.stats["encode_s"] += t1 - t0
