@@ -789,8 +789,9 @@ def bench_ffv1(args, rank, world, dev):
     dt = (time.perf_counter() - t0) / args.steps
     dt = batch_barrier.max_over_ranks(dt, world)
     raw = frame_bytes("yuv422p10le", w, h)
-    # decode of the same packets (host packets -> H2D -> one lane per slice)
-    pk = buf.cpu().numpy().tobytes()
+    # decode of the same packets (pinned host packets -> H2D -> one lane per
+    # slice), as Ffv1AviReader hands them over (read into a pinned buffer)
+    pk = buf.cpu().pin_memory().numpy()
     dec = ffv1.Ffv1Decoder(enc.extradata, w, h, max_frames=n, device=dev)
     back = FrameBatch("yuv422p10le", w, h, n, device=dev)
     dec.decode(pk, sizes, dst=back)

@@ -40,8 +40,8 @@ struct Ffv1DecArgs {
     int lpw;                     // slices (active lanes) per 64-lane workgroup: ffv1_lanes_per_wave()
     int debug;                   // PIXPATH_FFV1_DEBUG (timing ablation only; the output is wrong):
                                  // 8 no state-block loads, 16 no state-block stores
-    int64_t state_bytes;         // per slice: 2 * ctx_count * 32 + 64
-    uint8_t *states;             // [nslices][state_bytes], primed to 128
+    int64_t state_bytes;         // per slice: 2 * ctx_count * 32
+    uint8_t *states;             // [nslices / 64][2 * ctx_count][64][32], primed to 128
     int *status;
     const uint8_t *tables;       // zero[256], one[256], crc table
     const int16_t *quant;        // [3][256] (scaled)
@@ -170,7 +170,12 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
             return;
         }
     }
-    uint8_t *const st0 = a.states + (int64_t)g * a.state_bytes;
+    // context states of 64 neighbouring slices interleaved by slice (as the
+    // encoder's): context k of slice g at [g / 64][k][g % 64], so a context
+    // that is hot in neighbouring slices -- the same picture content -- shares
+    // their 128-B lines in L2 instead of one line per slice
+    uint8_t *const st0 = a.states + (int64_t)(g >> 6) * (64 * a.state_bytes) + (g & 63) * kCtx;
+    constexpr int kCtxStride = 64 * kCtx;
     Dec d;
     d.p = sb; d.end = sb + n; d.range = 0xFF00;
     d.low = n >= 2 ? ((uint32_t)sb[0] << 8) | sb[1] : 0;
@@ -229,8 +234,8 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
                 if (neg) ctx = -ctx;
                 const int key = key0 + ctx;
                 if (key != cur_key) {
-                    if (cur_key >= 0 && !(PP_ABLATE(a.debug) & 16)) dblk_store(st0 + cur_key * kCtx, blk);
-                    if (!(PP_ABLATE(a.debug) & 8)) dblk_load(blk, st0 + key * kCtx);
+                    if (cur_key >= 0 && !(PP_ABLATE(a.debug) & 16)) dblk_store(st0 + cur_key * kCtxStride, blk);
+                    if (!(PP_ABLATE(a.debug) & 8)) dblk_load(blk, st0 + key * kCtxStride);
                     cur_key = key;
                 }
                 int diff = dec_symbol<true>(d, blk, s_tab, bad);
@@ -284,7 +289,7 @@ extern "C" int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extra, int ext
     }
     const int64_t ns = (int64_t)D->nh * D->nv * max_frames;
     PP_HIP(hipSetDevice(ctx->device));
-    PP_HIP(hipMalloc(&D->states, (size_t)(2 * (int64_t)D->ctx_count * kCtx + 64) * ns));
+    PP_HIP(hipMalloc(&D->states, (size_t)(2 * (int64_t)D->ctx_count * kCtx) * ((ns + 63) / 64 * 64)));
     PP_HIP(hipMalloc(&D->soff, sizeof(int64_t) * ns));
     PP_HIP(hipMalloc(&D->slen, sizeof(int64_t) * ns));
     PP_HIP(hipMalloc(&D->status, sizeof(int) * ns));
@@ -346,8 +351,8 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     PP_HIP(hipMemcpyAsync(D->pkt, packets, base, hipMemcpyHostToDevice, st));
     PP_HIP(hipMemcpyAsync(D->soff, soff.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
     PP_HIP(hipMemcpyAsync(D->slen, slen.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
-    const int64_t sb = 2 * (int64_t)D->ctx_count * kCtx + 64;
-    PP_HIP(hipMemsetAsync(D->states, 128, (size_t)sb * ns, st));
+    const int64_t sb = 2 * (int64_t)D->ctx_count * kCtx;
+    PP_HIP(hipMemsetAsync(D->states, 128, (size_t)sb * ((ns + 63) / 64 * 64), st));
     Ffv1DecArgs a{};
     a.pkt = D->pkt; a.soff = D->soff; a.slen = D->slen;
     for (int p = 0; p < 3; ++p) {

@@ -68,8 +68,17 @@ template <int BITS>
 __device__ inline void store4(uint8_t *drow, int xo, const int o[4], bool vec, int dw) {
     if constexpr (BITS == 8) {
         if (vec) {
-            *reinterpret_cast<uint32_t *>(drow + xo) =
-                (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | ((uint32_t)o[3] << 24);
+            // opaque bytes: two clamped 8-bit results otherwise fold into
+            // v_ashr_pk_u8_i32, which leaves its destination's high half as it
+            // was, and the OR then keeps those stale bits in bytes 2 and 3
+            // (tests/test_gpu_chain.py caught it; cpvs.hip has the same guard)
+            uint32_t b[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                b[j] = (uint32_t)o[j];
+                asm volatile("" : "+v"(b[j]));
+            }
+            *reinterpret_cast<uint32_t *>(drow + xo) = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
         } else {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -118,6 +127,15 @@ template <int HW, int VTM>
 constexpr int strip_chain_min_waves() {
     return (HW <= 4 && VTM <= 3) ? 6 : ((HW <= 10 && VTM <= 5) || (HW == 12 && VTM <= 3)) ? 4 : 3;
 }
+// Instances with register room for the clamped V-pass copy (a second
+// instantiation of the row loop): the rest keep the per-lane path rather than
+// spill (tools/check_spills.sh: 8-bit sources into 8-bit rows with 4-dword
+// windows, chain plans with 10+ dword windows spilled 1-5 VGPRs with it).
+template <typename ST, int OUTB, int HW, int VTM, int FUSE>
+constexpr bool strip_clamp_path() {
+    return !(FUSE >= 8 && HW >= 10) && !(sizeof(ST) == 1 && OUTB == 8 && HW == 4 && (FUSE >= 8 || VTM >= 5));
+}
+
 template <typename ST, int OUTB, int HW, int VTM, int FUSE = 0, int TW = 256>
 __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() : strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
     static_assert(TW == 256 || TW == 512, "strip width");
@@ -435,8 +453,12 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
             default: if constexpr (VTM >= 8) vpass(std::integral_constant<int, 8>{}, cl_c); break;
             }
         };
-        if (clamp && FUSE != 1) vdispatch(std::true_type{});
-        else vdispatch(std::false_type{});
+        if constexpr (FUSE != 1 && strip_clamp_path<ST, OUTB, HW, VTM, FUSE>()) {
+            if (clamp) vdispatch(std::true_type{});
+            else vdispatch(std::false_type{});
+        } else {
+            vdispatch(std::false_type{});
+        }
         if constexpr (FUSE >= 8) {
             // ---- second stage (fuse 2): vertical filter of the ring2 rows ----
             if (jfuse == 2 && !(PP_ABLATE(a.debug) & 16)) {  // debug 16: no second stage (timing only)
@@ -498,8 +520,12 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                     default: pass2(std::integral_constant<int, 4>{}, cl_c); break;
                     }
                 };
-                if (clamp) dispatch2(std::true_type{});
-                else dispatch2(std::false_type{});
+                if constexpr (strip_clamp_path<ST, OUTB, HW, VTM, FUSE>()) {
+                    if (clamp) dispatch2(std::true_type{});
+                    else dispatch2(std::false_type{});
+                } else {
+                    dispatch2(std::false_type{});
+                }
             }
         }
         __builtin_amdgcn_s_setprio(0);

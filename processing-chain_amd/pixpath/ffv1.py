@@ -492,16 +492,34 @@ class Ffv1AviReader:
     def __len__(self):
         return len(self.index)
 
+    def _pinned(self, n):
+        """A page-locked host buffer of >= n bytes (reused): the decoder's H2D
+        of the packets then runs at DMA speed instead of through the driver's
+        pageable staging copy."""
+        if getattr(self, "_pin", None) is None or self._pin.numel() < n:
+            self._pin = torch.empty(max(int(n * 1.25), 1 << 20), dtype=torch.uint8).pin_memory()
+        return self._pin.numpy()
+
     def _read(self, i, m):
-        """Packets i..i+m-1 back to back (one read of their file span) and their sizes."""
+        """Packets i..i+m-1 back to back (read straight into a pinned buffer)
+        and their sizes."""
         ent = self.index[i:i + m]
         lo, hi = ent[0][0], ent[-1][0] + ent[-1][1]
-        self.fh.seek(lo)
-        span = np.frombuffer(self.fh.read(hi - lo), np.uint8)
         sizes = np.array([s for _, s in ent], np.int64)
-        if hi - lo == int(sizes.sum()):
-            return span, sizes
-        return np.concatenate([span[o - lo:o - lo + s] for o, s in ent]), sizes
+        total = int(sizes.sum())
+        buf = self._pinned(hi - lo)
+        self.fh.seek(lo)
+        got = self.fh.readinto(memoryview(buf)[:hi - lo])
+        if got != hi - lo:
+            raise ValueError("%s: truncated packet data" % self.fh.name)
+        if hi - lo == total:
+            return buf[:total], sizes
+        # chunk headers between the packets: close the gaps in place (moving left)
+        w = 0
+        for o, s in ent:
+            buf[w:w + s] = buf[o - lo:o - lo + s]
+            w += s
+        return buf[:total], sizes
 
     def read_device(self, n):
         """Up to n decoded frames as an interleaved device FrameBatch (None at

@@ -47,4 +47,7 @@ print("kernels with a private segment:", len(bad))
 PY
 # v_ashr_pk_u8_i32 keeps its destination's high half: a kernel that ORs more bytes
 # into such a result is wrong (cpvs.hip hit this); flag every occurrence
-grep -l "v_ashr_pk_u8_i32" /tmp/scale.s /tmp/cpvs.s /tmp/pack.s /tmp/siti.s /tmp/strip_u16.s /tmp/strip_u8.s && echo "v_ashr_pk_u8_i32 present: check its uses" || echo "no v_ashr_pk_u8_i32"
+if grep -l "v_ashr_pk_u8_i32" /tmp/scale.s /tmp/cpvs.s /tmp/pack.s /tmp/siti.s /tmp/strip_u16.s /tmp/strip_u8.s; then
+  echo "v_ashr_pk_u8_i32 present: check its uses"; exit 1
+fi
+echo "no v_ashr_pk_u8_i32"
