@@ -891,7 +891,10 @@ bool identity_bank(const pp::FilterBank &f, int one) {
 
 }  // namespace
 
-constexpr int kChainCho = 16;
+#ifndef PIXPATH_CHAIN_CHO
+#define PIXPATH_CHAIN_CHO 16
+#endif
+constexpr int kChainCho = PIXPATH_CHAIN_CHO;
 
 // create_avpvs_segment's two stages (lib/ffmpeg.py:1037-1048): the scale
 // filter writes the overlay's yuv420p (overlay's default format=yuv420), then
@@ -975,7 +978,15 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
         }
         ring2 = (ring2 + 1) & ~1;
     }
+#ifdef PIXPATH_RING2_WORDS
     const size_t lds = P->fast_lds + (size_t)ring2 * P->fast_tw * 2;
+    const int r2rows = ring2;
+#else
+    // the byte ring is circular: a power of two of rows >= every chunk's live span
+    int r2rows = 2;
+    while (r2rows < ring2) r2rows <<= 1;
+    const size_t lds = P->fast_lds + (ring2 ? (size_t)r2rows * P->fast_tw : 0);
+#endif
     if (!ok || lds > 64 * 1024) {
         *out = P.release();
         return PP_OK;
@@ -998,6 +1009,7 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
         J.fuse = (p && v422) ? 2 : widen;
         if (J.fuse == 2) {
             J.vtp2 = vtp2;
+            J.r2mask = r2rows - 1;
             J.vrow2 = static_cast<const int32_t *>(P->dev2);
             J.chunk2 = reinterpret_cast<const int32_t *>(static_cast<uint8_t *>(P->dev2) + b1);
         }

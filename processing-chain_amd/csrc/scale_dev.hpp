@@ -64,6 +64,7 @@ struct PlaneJob {
     // chain plans (strip_kernel FUSE != 0, see strip.hpp)
     int fuse;               // 0 as is, 1 identity second stage, 2 second-stage vertical filter through ring2
     int vtp2;               // second-stage V tap pairs (fuse 2)
+    int r2mask;             // fuse 2: rows of the circular byte ring2 - 1 (a power of two)
     const int32_t *vrow2;   // [dh2][16] second-stage row records (base row, tap pairs)
     const int32_t *chunk2;  // [nch][4] per chunk: second-stage rows [lo2, hi2), ring2 base row, kept pairs
     int pk_off, pk_step;    // strip_kernel FUSE == 1: byte offset / step of this plane in the uyvy422 row

@@ -163,7 +163,14 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
     const int cx = (tid & (TW / 4 - 1)) * 4;
     uint16_t *src_t = lds;                                                  // [maxnew][S]
     uint32_t *win = reinterpret_cast<uint32_t *>(lds + J.maxnew * S);       // [ring/2][TW] row pairs
+#ifdef PIXPATH_RING2_WORDS
     uint32_t *ring2 = win + (J.ring >> 1) * TW;                             // FUSE, fuse 2: [ring2/2][TW]
+#else
+    // FUSE, fuse 2: the second stage's input rows as bytes, a circular ring of
+    // J.r2mask + 1 rows ([row & r2mask][TW] bytes): a lane stores its 4 bytes
+    // of a row in one conflict-free dword, and no row is ever moved
+    uint8_t *ring2b = reinterpret_cast<uint8_t *>(win + (J.ring >> 1) * TW);
+#endif
     const kconst int32_t *chunk2 = as_kconst<int32_t>(J.chunk2);            // [nch][4]: lo2, hi2, base2, keep2
     const ST *sbase = reinterpret_cast<const ST *>(a.src[p] + frame * a.sfs[p]);
     uint8_t *dbase = a.dst[p] + frame * a.dfs[p];
@@ -294,6 +301,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
             for (int k = 0; k < keep; ++k) win[k * TW + tid] = win[(k + shift) * TW + tid];
             moved = true;
         }
+#ifdef PIXPATH_RING2_WORDS
         int base2 = 0;
         if constexpr (FUSE >= 8) {
             if (J.fuse == 2) {  // ring2 keeps the rows the pending second-stage outputs still read
@@ -305,6 +313,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                 }
             }
         }
+#endif
         if (moved) __syncthreads();
         base = nbase;
         // ---- horizontal pass: row pairs of the window, wave-strided ----------
@@ -409,10 +418,21 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
 #pragma unroll
                     for (int j = 0; j < 4; ++j) o[j] = min(max(acc[j] >> sh, 0), mx);
                     if constexpr (FUSE >= 8) {
-                        if (jfuse == 2) {  // into ring2 (second-stage input), 15-bit
+                        if (jfuse == 2) {  // into ring2 (second-stage input)
+#ifdef PIXPATH_RING2_WORDS
                             uint16_t *r16 = reinterpret_cast<uint16_t *>(ring2 + ((y - base2) >> 1) * TW + vx);
 #pragma unroll
                             for (int j = 0; j < 4; ++j) r16[2 * j + (y & 1)] = static_cast<uint16_t>(o[j] << 7);
+#else
+                            uint32_t bq[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {  // opaque bytes (v_ashr_pk_u8_i32, see store4)
+                                bq[j] = (uint32_t)o[j];
+                                asm volatile("" : "+v"(bq[j]));
+                            }
+                            *reinterpret_cast<uint32_t *>(ring2b + (y & J.r2mask) * TW + vx) =
+                                bq[0] | (bq[1] << 8) | (bq[2] << 16) | (bq[3] << 24);
+#endif
                             __builtin_amdgcn_sched_barrier(0);
                             continue;
                         }
@@ -487,13 +507,35 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                         for (int i = 0; i < G2; ++i) {
                             const int r2 = g0 + 4 * i;
                             if (r2 >= hi2) break;
+                            int acc[4];
+#ifdef PIXPATH_RING2_WORDS
                             const uint4 *rp = reinterpret_cast<const uint4 *>(ring2 + ((vb[i] - base2) >> 1) * TW + vx);
                             uint4 q[VT2];
 #pragma unroll
                             for (int j = 0; j < VT2; ++j) q[j] = rp[j * (TW / 4)];
-                            int acc[4];
 #pragma unroll
                             for (int j = 0; j < 4; ++j) acc[j] = FUSE == 8 ? 64 << 12 : 1 << (10 + 16 - FUSE);
+#else
+                            // rows vb + 2j, vb + 2j + 1 from the byte ring, interleaved into
+                            // the (row, row + 1) sample pairs of v_dot2; the first stage's
+                            // << 7 (hScale8To15 of the identity H filter) moves onto the sum
+                            uint32_t ra[VT2], rb[VT2];
+#pragma unroll
+                            for (int j = 0; j < VT2; ++j) {
+                                ra[j] = *reinterpret_cast<const uint32_t *>(ring2b + ((vb[i] + 2 * j) & J.r2mask) * TW + vx);
+                                rb[j] = *reinterpret_cast<const uint32_t *>(ring2b + ((vb[i] + 2 * j + 1) & J.r2mask) * TW + vx);
+                            }
+                            uint4 q[VT2];
+#pragma unroll
+                            for (int j = 0; j < VT2; ++j) {
+                                q[j].x = __builtin_amdgcn_perm(rb[j], ra[j], 0x0c040c00u);
+                                q[j].y = __builtin_amdgcn_perm(rb[j], ra[j], 0x0c050c01u);
+                                q[j].z = __builtin_amdgcn_perm(rb[j], ra[j], 0x0c060c02u);
+                                q[j].w = __builtin_amdgcn_perm(rb[j], ra[j], 0x0c070c03u);
+                            }
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) acc[j] = 0;
+#endif
 #pragma unroll
                             for (int j = 0; j < VT2; ++j) {
                                 const v2i16 c2 = __builtin_bit_cast(v2i16, cf[i][j]);
@@ -502,6 +544,10 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                                 acc[2] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].z), c2, acc[2], false);
                                 acc[3] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].w), c2, acc[3], false);
                             }
+#ifndef PIXPATH_RING2_WORDS
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) acc[j] = (acc[j] << 7) + (FUSE == 8 ? 64 << 12 : 1 << (10 + 16 - FUSE));
+#endif
                             if (!CL && !lane_any) continue;
                             constexpr int s2 = FUSE == 8 ? 19 : 11 + 16 - FUSE;
                             int w[4];

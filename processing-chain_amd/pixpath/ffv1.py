@@ -99,19 +99,26 @@ class Ffv1Encoder:
             check(lib().pp_stream_synchronize(st))
         return out[:total], sizes
 
+    def packets_to_host(self, ptr, n, stream):
+        """One D2H of the last encode's n packet bytes (device pointer ptr) into
+        the encoder's pinned host buffer on `stream`; returns its numpy view
+        (valid until the next call)."""
+        if getattr(self, "_host", None) is None or self._host.numel() < n:
+            self._host = torch.empty(max(n + n // 4, 1 << 20), dtype=torch.uint8).pin_memory()
+        if n:
+            st = ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+            check(lib().pp_copy_async(ctypes.c_void_p(self._host.data_ptr()), ctypes.c_void_p(ptr), n, PP_COPY_D2H,
+                                      st))
+            check(lib().pp_stream_synchronize(st))
+        return self._host[:n].numpy()
+
     def encode_host(self, src, stream=None):
         """(numpy uint8 view of the packets in a pinned host buffer, frame sizes):
         encode, then one D2H of the packets straight from the encoder's packet
         buffer (valid until the next call)."""
         ptr, n, sizes = self.encode_packets(src, stream)
-        if getattr(self, "_host", None) is None or self._host.numel() < n:
-            self._host = torch.empty(max(n + n // 4, 1 << 20), dtype=torch.uint8).pin_memory()
-        if n:
-            st = _stream(src.planes[0], stream)
-            check(lib().pp_copy_async(ctypes.c_void_p(self._host.data_ptr()), ctypes.c_void_p(ptr), n, PP_COPY_D2H,
-                                      st))
-            check(lib().pp_stream_synchronize(st))
-        return self._host[:n].numpy(), sizes
+        st = stream if stream is not None else torch.cuda.current_stream(src.device)
+        return self.packets_to_host(ptr, n, st), sizes
 
     def encode_to_host(self, src, stream=None):
         """List of per-frame packets (bytes)."""
@@ -348,11 +355,14 @@ class Ffv1AviWriter:
                     ev.synchronize()  # the frames of this batch are in the staging batch
                     src = FrameBatch.interleaved(self.fmt, self.w, self.h, n, device=self.device,
                                                  storage=self.enc.stages[slot].storage[:n])
-                    with self.lock:
+                    with self.lock:  # the device's encodes one at a time, on its encode stream
                         t0 = time.perf_counter()
                         with torch.cuda.stream(self.stream):
-                            data, sizes = self.enc.encode_host(src, stream=self.stream)
-                        t1 = time.perf_counter()
+                            ptr, n, sizes = self.enc.encode_packets(src, stream=self.stream)
+                    # the packets leave on the copy stream, outside the lock: the
+                    # next writer's encode starts while this D2H runs
+                    data = self.enc.packets_to_host(ptr, n, self.put_stream)
+                    t1 = time.perf_counter()
                     self.avi.write_packets(data, sizes)
                     t2 = time.perf_counter()
                     self.stats["encode_s"] += t1 - t0
