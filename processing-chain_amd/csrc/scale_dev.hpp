@@ -17,8 +17,14 @@ namespace pp {
 constexpr int kTileW = 256;      // widest output tile (columns); narrower for large downscales
 constexpr int kThreads = 256;    // 4 waves
 constexpr int kLdsBudget = 40 * 1024;
-constexpr int kChoMax = 32;     // output rows per chunk (upper bound)
-constexpr int kSegRows = 540;   // output rows per segment (target; profiles/r2: 540 beats 256 by ~1.5 %)
+#ifndef PIXPATH_CHO_MAX
+#define PIXPATH_CHO_MAX 32
+#endif
+#ifndef PIXPATH_SEG_ROWS
+#define PIXPATH_SEG_ROWS 540
+#endif
+constexpr int kChoMax = PIXPATH_CHO_MAX;    // output rows per chunk (upper bound)
+constexpr int kSegRows = PIXPATH_SEG_ROWS;  // output rows per segment (target; profiles/r2: 540 beats 256 by ~1.5 %)
 
 static __constant__ uint8_t c_dither[8][8] = {
     {36, 68, 60, 92, 34, 66, 58, 90},  {100, 4, 124, 28, 98, 2, 122, 26},

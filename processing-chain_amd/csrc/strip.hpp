@@ -133,6 +133,9 @@ constexpr int strip_chain_min_waves() {
 // windows, chain plans with 10+ dword windows spilled 1-5 VGPRs with it).
 template <typename ST, int OUTB, int HW, int VTM, int FUSE>
 constexpr bool strip_clamp_path() {
+#ifdef PIXPATH_NO_CLAMP_PLAIN
+    if (FUSE == 0) return false;
+#endif
     return !(FUSE >= 8 && HW >= 10) && !(sizeof(ST) == 1 && OUTB == 8 && HW == 4 && (FUSE >= 8 || VTM >= 5));
 }
 
@@ -354,7 +357,9 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
         // ---- vertical pass: one output row per wave --------------------------
         // raised priority while the wave issues its output rows: the other
         // waves' H pass never starves the write stream (-2 %, profiles/r2)
+#ifndef PIXPATH_NO_SETPRIO
         __builtin_amdgcn_s_setprio(1);
+#endif
         const int ny = min(cho, y_end - y0);
         // VT (= vtp) tap pairs, compile-time per instance: every window read of
         // a row is in flight before the first v_dot2 waits on one
@@ -365,7 +370,11 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
             // row records (window base row + VT tap pairs) of G rows at a time
             // through the scalar cache: one exposed scalar-load latency per
             // group, not per row (the ds_reads of a row depend on its base)
+#ifdef PIXPATH_VPASS_G8
+            constexpr int G = VT <= 5 ? 8 : 4;
+#else
             constexpr int G = VT <= 2 ? 8 : VT <= 5 ? 4 : 2;
+#endif
             for (int g0 = rg; g0 < ny; g0 += 4 * G) {
                 int vb[G];
                 int32_t cf[G][VT];

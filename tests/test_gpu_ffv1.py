@@ -407,7 +407,7 @@ def test_failed_writer_leaves_no_file_and_frees_its_encoder(gpu, tmp_path, monke
 
     def boom(*a, **k):
         raise RuntimeError("injected encode failure")
-    monkeypatch.setattr(enc, "encode_host", boom)
+    monkeypatch.setattr(enc, "encode_packets", boom)
     src = FrameBatch.interleaved("yuv422p10le", 320, 180, 3, device=gpu)
     src.storage.zero_()
     wr.write_device(src)
