@@ -162,7 +162,6 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
     // row group (H-pass row pairs and V-pass rows strided by 4); at TW = 512
     // waves 2r and 2r+1 are row group r, left and right 256 columns
     const int rg = TW == 512 ? wave >> 1 : wave;
-    const int lane = tid & 63;
     const int cx = (tid & (TW / 4 - 1)) * 4;
     uint16_t *src_t = lds;                                                  // [maxnew][S]
     uint32_t *win = reinterpret_cast<uint32_t *>(lds + J.maxnew * S);       // [ring/2][TW] row pairs
@@ -610,10 +609,18 @@ inline int strip_vtm_bucket_impl(int vtp) { return vtp <= 2 ? 2 : vtp <= 3 ? 3 :
     default: return nullptr;                                                 \
     }
 #define PP_STRIP_HW_F(ST, OUTB, FUSE) PP_STRIP_HW_FT(ST, OUTB, FUSE, 256)
+// 512-column strips are reachable only through the PIXPATH_STRIP_TW knob of
+// the measurement build (scale.hip plan_create), so only it instantiates them
+#ifdef PIXPATH_ABLATE
 #define PP_STRIP_HW(ST, OUTB)                                                \
     if (tw == 512) {                                                         \
         PP_STRIP_HW_FT(ST, OUTB, 0, 512)                                     \
     }                                                                        \
     PP_STRIP_HW_FT(ST, OUTB, 0, 256)
+#else
+#define PP_STRIP_HW(ST, OUTB)                                                \
+    (void)tw;                                                                \
+    PP_STRIP_HW_FT(ST, OUTB, 0, 256)
+#endif
 
 }  // namespace pp

@@ -1,4 +1,6 @@
-// strip_kernel instances for 16-bit (9/10-bit) source samples (see strip.hpp).
+// strip_kernel instances for 16-bit (9/10-bit) source samples, plain plans (see
+// strip.hpp); the chain and packed instances are in strip_u16_chain.hip, so the
+// two units compile in parallel.
 #include "strip.hpp"
 
 namespace pp {
@@ -11,16 +13,5 @@ KernelFn pick_strip_u16(int outb, int hw, int vtm, int tw) {
 }
 
 int strip_vtm_bucket(int vtp) { return strip_vtm_bucket_impl(vtp); }
-
-KernelFn pick_strip_chain_u16(int out2, int hw, int vtm) {
-    if (out2 == 8) {
-        PP_STRIP_HW_F(uint16_t, 8, 8)
-    }
-    PP_STRIP_HW_F(uint16_t, 8, 10)
-}
-
-KernelFn pick_strip_packed_u16(int hw, int vtm) {
-    PP_STRIP_HW_F(uint16_t, 8, 1)
-}
 
 }  // namespace pp

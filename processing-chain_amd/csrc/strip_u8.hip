@@ -1,4 +1,6 @@
-// strip_kernel instances for 8-bit source samples (see strip.hpp).
+// strip_kernel instances for 8-bit source samples, plain plans (see
+// strip.hpp); the chain and packed instances are in strip_u8_chain.hip, so the
+// two units compile in parallel.
 #include "strip.hpp"
 
 namespace pp {
@@ -8,17 +10,6 @@ KernelFn pick_strip_u8(int outb, int hw, int vtm, int tw) {
         PP_STRIP_HW(uint8_t, 8)
     }
     PP_STRIP_HW(uint8_t, 10)
-}
-
-KernelFn pick_strip_chain_u8(int out2, int hw, int vtm) {
-    if (out2 == 8) {
-        PP_STRIP_HW_F(uint8_t, 8, 8)
-    }
-    PP_STRIP_HW_F(uint8_t, 8, 10)
-}
-
-KernelFn pick_strip_packed_u8(int hw, int vtm) {
-    PP_STRIP_HW_F(uint8_t, 8, 1)
 }
 
 }  // namespace pp

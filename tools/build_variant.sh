@@ -5,7 +5,7 @@ set -e
 name=$1; defs=$2
 cd "$(dirname "$0")/../processing-chain_amd"
 out=build/var_$name; mkdir -p $out ../tools/ablate
-for f in scale.hip strip_u16.hip strip_u8.hip; do
+for f in scale.hip strip_u16.hip strip_u16_chain.hip strip_u8.hip strip_u8_chain.hip; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result $defs -x hip -c csrc/$f -o $out/$f.o &
 done
 wait

@@ -27,3 +27,10 @@ for wl in config3-10 config3-8 config4; do
   timeout -k 10 200 python -u bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline --no-pipeline > gpurun_out/bench_${wl}_$TAG.json 2>> gpurun_out/bench_$TAG.err || { tail -3 gpurun_out/bench_$TAG.err; exit 1; }
   cut -c1-200 gpurun_out/bench_${wl}_$TAG.json
 done
+# config-4 chain instruction mix (SALU below VALU) and config-3 8-bit LDS conflicts
+for wl in config4 config3-8; do
+  mkdir -p gpurun_out/mix_${wl}_$TAG
+  if [ $wl = config4 ]; then A="--workload config4 --steps 1 --warmup 0 --no-cpu-baseline"; else A="--workload config3-8 --steps 1 --warmup 0 --pvs-total 2 --pool 2 --no-cpu-baseline --no-pipeline --no-siti-file --no-e2e"; fi
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/mix_${wl}_$TAG/p1 -o run -- python3 bench.py $A > gpurun_out/mix_${wl}_$TAG/p1.log 2>&1 || { echo "mix pass $wl failed"; tail -5 gpurun_out/mix_${wl}_$TAG/p1.log; exit 1; }
+  echo "### $wl"; python3 tools/summarize_counters.py gpurun_out/mix_${wl}_$TAG | grep -A12 "strip_kernel" > gpurun_out/mix_${wl}_$TAG.txt; cat gpurun_out/mix_${wl}_$TAG.txt
+done
