@@ -15,10 +15,22 @@ from ._native import pp_frames
 
 import os
 
-# layout padding for measurement (bytes added to every row pitch, rows added
-# to every plane of a frame); the kernels take any pitch / frame stride
-_PITCH_PAD = int(os.environ.get("PIXPATH_PITCH_PAD", "0"))
-_ROWS_PAD = int(os.environ.get("PIXPATH_ROWS_PAD", "0"))
+from . import _native
+
+
+def _layout_pad():
+    """Layout padding for measurements (tools/gpu_pad_sweep.sh: bytes added to
+    every row pitch, rows added to every plane of a frame; the kernels take any
+    pitch / frame stride).  Read only when a library other than the product's
+    is loaded (PIXPATH_LIB = the measurement build), like the library's own
+    knobs: the product layout never depends on the environment."""
+    if os.path.realpath(_native.LIB_PATH) == os.path.realpath(os.path.join(os.path.dirname(_native.__file__),
+                                                                          "libpixpath.so")):
+        return 0, 0
+    return int(os.environ.get("PIXPATH_PITCH_PAD", "0")), int(os.environ.get("PIXPATH_ROWS_PAD", "0"))
+
+
+_PITCH_PAD, _ROWS_PAD = _layout_pad()
 
 
 def _pitch(cols, bps, align=16):

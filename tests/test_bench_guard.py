@@ -50,3 +50,17 @@ def test_product_library_reads_no_knobs():
     for knob in (b"PIXPATH_SCALE_DEBUG", b"PIXPATH_FFV1_DEBUG", b"PIXPATH_STRIP_TW", b"PIXPATH_SCALE_LDS_KB",
                  b"PIXPATH_FFV1_LPW", b"PIXPATH_CHAIN_LUMA_CHO", b"PIXPATH_SCALE_KERNEL", b"getenv"):
         assert knob not in data, knob
+
+
+def test_layout_padding_ignored_by_the_product_library():
+    """The frame-layout padding knobs (tools/gpu_pad_sweep.sh) take effect only
+    with the measurement build loaded; with the product library the layout is
+    the unpadded one whatever the environment says."""
+    code = ("import sys; sys.path.insert(0, %r); from pixpath import frames; "
+            "print(frames._PITCH_PAD, frames._ROWS_PAD, frames._pitch(1920, 2))"
+            % os.path.join(ROOT, "processing-chain_amd"))
+    env = {k: v for k, v in os.environ.items() if not k.startswith("PIXPATH_")}
+    env.update({"PIXPATH_PITCH_PAD": "256", "PIXPATH_ROWS_PAD": "3"})
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["0", "0", "1920"]
