@@ -36,7 +36,8 @@ def main():
     sizes = np.asarray(sizes, dtype=np.int64)
     offs = np.concatenate([[0], np.cumsum(sizes)])
     dec = ffv1.Ffv1Decoder(enc.extradata, w, h, max_frames=n, device=dev)
-    for K in (600, 300, 200, 150, 100, 60):
+    ks = [int(a) for a in sys.argv[1:]] or [600, 300, 200, 150, 100, 60]
+    for K in ks:
         outs = [FrameBatch("yuv422p10le", w, h, min(K, n - k0), device=dev) for k0 in range(0, n, K)]
 
         def run():

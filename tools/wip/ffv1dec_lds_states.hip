@@ -2,19 +2,25 @@
 // half): reads AVPVS frame packets back into planar frames in HBM for the
 // CPVS stage (create_cpvs decodes the FFV1 AVPVS, lib/ffmpeg.py:1149-1201).
 //
-// Same shape as the encoder (ffv1.hip): ONE LANE PER SLICE over every slice of
-// every frame of the batch.  The host walks each packet's slice footers
-// backwards (24-bit sizes, RFC 9043 4.8) into a slice table; a lane checks
-// its slice's CRC-32 parity, reads the keyframe bit (first slice), the slice
-// header (position from the header, as FFmpeg's decode_slice_header), then
-// decodes Y, Cb, Cr in raster order -- quantised context from the record's
-// tables (LDS), median prediction, get_symbol through the slice's own context
-// states (current context cached in LDS, as in the encoder) -- writing each
-// sample straight into the destination planes, whose previous row it reads
-// back for T / TL / TR.  It finishes with the closing bit at state 129 and
-// FFmpeg's end-of-slice position check.  Per-slice status: 0 ok, 1 CRC,
-// 2 header, 3 end mismatch.
+// One lane per slice over every slice of every frame of the batch, a
+// one-wave workgroup holding `lpw` slices (default 1).  The host walks each
+// packet's slice footers backwards (24-bit sizes, RFC 9043 4.8) into a slice
+// table; a lane checks its slice's CRC-32 parity, reads the keyframe bit
+// (first slice), the slice header (position from the header, as FFmpeg's
+// decode_slice_header), then decodes Y, Cb, Cr in raster order -- quantised
+// context from the record's tables, median prediction, get_symbol through the
+// slice's context states -- writing each sample into the destination planes
+// and into an LDS line buffer that supplies T / TL / TR for the next row.
+// Every frame is a keyframe, so a plane set's states start at 128: the 16
+// state bytes a residual below 32 touches live in LDS for the active plane
+// set (primed in place), the other 16 per context in HBM.  The sample chain
+// (context -> state block -> decisions -> sample -> next context) then runs
+// on LDS latency instead of an HBM/MALL round trip per sample (round 3's
+// 32-byte HBM blocks: ~1.85k frames/s on the bench content).  It finishes
+// with the closing bit at state 129 and FFmpeg's end-of-slice position check.
+// Per-slice status: 0 ok, 1 CRC, 2 header, 3 end mismatch.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -27,8 +33,8 @@ namespace pp {
 
 namespace {
 
-constexpr int kCtx = kFfv1CtxBytes;
-constexpr size_t kLineLds = 160 * 1024 - 4096;  // LDS left for line buffers (gfx950: 160 KB per CU)
+constexpr size_t kLdsBytes = 160 * 1024;  // gfx950 LDS per CU (one workgroup may take all of it)
+constexpr size_t kFixedLds = 2048 + 128;  // state tables, quantisers, CRC shift powers
 
 }  // namespace
 
@@ -39,24 +45,19 @@ struct Ffv1DecArgs {
     int64_t ls[3], fs[3];
     int w, h, bytes, bits, hsub, vsub, nh, nv, nslices, ec;
     int ctx_count;               // contexts per plane set (record's tables)
-    int lpw;                     // slices (active lanes) per 64-lane workgroup: ffv1_lanes_per_wave()
-    int row_cap;                 // samples per lane in the LDS line buffer (>= widest slice row)
-    int debug;                   // PIXPATH_FFV1_DEBUG (timing ablation only; the output is wrong):
-                                 // 2 no CRC check, 8 no state-block loads, 16 no state-block stores
-    int64_t state_bytes;         // per slice: 2 * ctx_count * 32
-    uint8_t *states;             // [nslices / 64][2 * ctx_count][64][32], primed to 128
+    int lpw;                     // slices (active lanes) per one-wave workgroup
+    int row_cap;                 // samples per lane in the LDS row buffer (>= widest slice row)
+    uint8_t *cold;               // [nslices][2 * ctx_count + 1][16] cold state bytes, primed to 128
     int *status;
     const uint8_t *tables;       // zero[256], one[256], crc table
     const int16_t *quant;        // [3][256] (scaled)
+    int debug;                   // PIXPATH_FFV1_DEBUG (ablation build; the output is wrong):
+                                 // 1 stop after the CRCs and headers, 2 skip the CRCs
 };
 
-// The slice's range decoder (rangecoder.h get_rac / refill) on register-held
-// state: a symbol's state bytes come from the current context's 32-byte block
-// in 8 VGPRs (all read before its first decision, updated bytes written after
-// the last, so the LDS state-table lookups never sit on the low/range chain).
-// The bytestream is read a dword at a time through a two-word register
-// window, the next word loaded four refills before it is needed, so no refill
-// waits on memory.
+// The slice's range decoder (rangecoder.h get_rac / refill).  The bytestream
+// is read a dword at a time through a two-word register window, the next word
+// loaded four refills before it is needed, so no refill waits on memory.
 struct Dec {
     uint32_t low, range;
     int pos, end;  // byte positions relative to the dword-aligned base `w`
@@ -91,68 +92,95 @@ __device__ __forceinline__ uint32_t dec_rac(Dec &d, uint32_t s, const uint8_t *t
     return bit;
 }
 
-__device__ __forceinline__ uint32_t dsget(const uint32_t (&b)[8], int k) { return (b[k >> 2] >> ((k & 3) * 8)) & 0xFFu; }
-__device__ __forceinline__ void dsput(uint32_t (&b)[8], int k, uint32_t v) {
+// A context's 32 state bytes split in two 16-byte halves.  HOT (in LDS, one
+// block per context of the active plane set): [0] zero flag, [1..5] exponent
+// bits 0..4, [6..10] sign for e = 0..4, [11..14] mantissa bits 0..3 -- every
+// state a residual below 32 in magnitude touches.  COLD (HBM, per slice):
+// [0..4] exponent bits 5..9, [5..9] sign for e = 5..9, [10..14] mantissa bits
+// 4..8, loaded only once a symbol's exponent reaches 5.
+__device__ __forceinline__ uint32_t bget(const uint32_t (&b)[4], int k) { return (b[k >> 2] >> ((k & 3) * 8)) & 0xFFu; }
+__device__ __forceinline__ void bput(uint32_t (&b)[4], int k, uint32_t v) {
     b[k >> 2] = (b[k >> 2] & ~(0xFFu << ((k & 3) * 8))) | (v << ((k & 3) * 8));
 }
-__device__ __forceinline__ uint32_t dsget_dyn(const uint32_t (&b)[8], int k) {  // k in 8..23
-    const int w = k >> 2;
-    const uint32_t x = w == 2 ? b[2] : w == 3 ? b[3] : w == 4 ? b[4] : b[5];
-    return (x >> ((k & 3) * 8)) & 0xFFu;
-}
-__device__ __forceinline__ void dsput_dyn(uint32_t (&b)[8], int k, uint32_t v) {
-    const int w = k >> 2;
-    const uint32_t sh = (k & 3) * 8, m = ~(0xFFu << sh), nv = v << sh;
-    b[2] = w == 2 ? (b[2] & m) | nv : b[2];
-    b[3] = w == 3 ? (b[3] & m) | nv : b[3];
-    b[4] = w == 4 ? (b[4] & m) | nv : b[4];
-    b[5] = w == 5 ? (b[5] & m) | nv : b[5];
-}
 
-// get_symbol (ffv1dec.c) for samples of <= 10 bits: exponent e <= 9, so
-// every state index is used at most once per symbol; e >= 10 (not a <= 10-bit
-// stream) sets `bad`.
+// get_symbol (ffv1dec.c) for samples of <= 10 bits: exponent e <= 9, so every
+// state index is used at most once per symbol; e >= 10 (not a <= 10-bit
+// stream) sets `bad`.  Decisions read the block as loaded and write the next
+// states into a copy, so no decision waits on the previous one's state-table
+// lookup (neighbouring state bytes share a dword).
 template <bool SIGNED>
-__device__ __forceinline__ int dec_symbol(Dec &d, uint32_t (&b)[8], const uint8_t *tab, bool &bad) {
-    uint32_t n0;
-    const uint32_t z = dec_rac(d, dsget(b, 0), tab, n0);
-    uint32_t nu[10], nm[9], nsg = 0;
+__device__ __forceinline__ int dec_symbol(Dec &d, uint32_t (&h)[4], uint8_t *cold, const uint8_t *tab, bool &bad) {
+    const uint32_t h0[4] = {h[0], h[1], h[2], h[3]};
+    uint32_t ns;
+    const uint32_t z = dec_rac(d, bget(h0, 0), tab, ns);
+    bput(h, 0, ns);
+    if (z) return 0;
     int e = 0, a = 1;
-    uint32_t neg = 0;
-    if (!z) {
-        bool go = true;
+    bool go = true;
 #pragma unroll
-        for (int i = 0; i < 10; ++i)
+    for (int i = 0; i < 5; ++i)
+        if (go) {
+            const uint32_t bit = dec_rac(d, bget(h0, 1 + i), tab, ns);
+            bput(h, 1 + i, ns);
+            if (bit) e = i + 1;
+            else go = false;
+        }
+    uint32_t neg;
+    if (go) {  // e >= 5: the cold half
+        const uint4 x = *reinterpret_cast<const uint4 *>(cold);
+        const uint32_t c0[4] = {x.x, x.y, x.z, x.w};
+        uint32_t c[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int i = 5; i < 10; ++i)
             if (go) {
-                if (dec_rac(d, dsget(b, 1 + i), tab, nu[i])) e = i + 1;
+                const uint32_t bit = dec_rac(d, bget(c0, i - 5), tab, ns);
+                bput(c, i - 5, ns);
+                if (bit) e = i + 1;
                 else go = false;
             }
         if (go) bad = true;
 #pragma unroll
-        for (int i = 8; i >= 0; --i)
-            if (i < e) a = 2 * a + (int)dec_rac(d, dsget(b, 22 + i), tab, nm[i]);
-        if constexpr (SIGNED) neg = dec_rac(d, dsget_dyn(b, 11 + min(e, 9)), tab, nsg);
-    }
-    dsput(b, 0, n0);
-    if (!z) {
+        for (int i = 8; i >= 4; --i)
+            if (i < e) {
+                a = 2 * a + (int)dec_rac(d, bget(c0, 10 + i - 4), tab, ns);
+                bput(c, 10 + i - 4, ns);
+            }
 #pragma unroll
-        for (int i = 0; i < 10; ++i)
-            if (i <= e) dsput(b, 1 + i, nu[i]);
+        for (int i = 3; i >= 0; --i) {
+            a = 2 * a + (int)dec_rac(d, bget(h0, 11 + i), tab, ns);
+            bput(h, 11 + i, ns);
+        }
+        neg = 0;
+        if constexpr (SIGNED) {
+            const int k = min(e, 9);  // sign state 5 + (k - 5) of the cold half
+            const uint32_t sv = k == 5 ? bget(c0, 5) : k == 6 ? bget(c0, 6) : k == 7 ? bget(c0, 7) : k == 8 ? bget(c0, 8) : bget(c0, 9);
+            neg = dec_rac(d, sv, tab, ns);
+            if (k == 5) bput(c, 5, ns);
+            else if (k == 6) bput(c, 6, ns);
+            else if (k == 7) bput(c, 7, ns);
+            else if (k == 8) bput(c, 8, ns);
+            else bput(c, 9, ns);
+        }
+        *reinterpret_cast<uint4 *>(cold) = make_uint4(c[0], c[1], c[2], c[3]);
+    } else {
 #pragma unroll
-        for (int i = 0; i < 9; ++i)
-            if (i < e) dsput(b, 22 + i, nm[i]);
-        if constexpr (SIGNED) dsput_dyn(b, 11 + min(e, 9), nsg);
+        for (int i = 3; i >= 0; --i)
+            if (i < e) {
+                a = 2 * a + (int)dec_rac(d, bget(h0, 11 + i), tab, ns);
+                bput(h, 11 + i, ns);
+            }
+        neg = 0;
+        if constexpr (SIGNED) {  // sign state 6 + e, e in 0..4
+            const uint32_t sv = e == 0 ? bget(h0, 6) : e == 1 ? bget(h0, 7) : e == 2 ? bget(h0, 8) : e == 3 ? bget(h0, 9) : bget(h0, 10);
+            neg = dec_rac(d, sv, tab, ns);
+            if (e == 0) bput(h, 6, ns);
+            else if (e == 1) bput(h, 7, ns);
+            else if (e == 2) bput(h, 8, ns);
+            else if (e == 3) bput(h, 9, ns);
+            else bput(h, 10, ns);
+        }
     }
-    return z ? 0 : (neg ? -a : a);
-}
-
-__device__ __forceinline__ void dblk_load(uint32_t (&b)[8], const uint8_t *p) {
-    const uint4 x = reinterpret_cast<const uint4 *>(p)[0], y = reinterpret_cast<const uint4 *>(p)[1];
-    b[0] = x.x; b[1] = x.y; b[2] = x.z; b[3] = x.w; b[4] = y.x; b[5] = y.y; b[6] = y.z; b[7] = y.w;
-}
-__device__ __forceinline__ void dblk_store(uint8_t *p, const uint32_t (&b)[8]) {
-    reinterpret_cast<uint4 *>(p)[0] = make_uint4(b[0], b[1], b[2], b[3]);
-    reinterpret_cast<uint4 *>(p)[1] = make_uint4(b[4], b[5], b[6], b[7]);
+    return neg ? -a : a;
 }
 
 // a(x) b(x) mod P for the slice CRC's polynomial (CRC-32 IEEE, MSB first)
@@ -168,24 +196,38 @@ __device__ __forceinline__ uint32_t gf2_mulmod(uint32_t a, uint32_t b) {
 
 __device__ __forceinline__ int dmedian3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 
+// One workgroup = one wave whose first `lpw` lanes decode a slice each.  LDS:
+// the tables, then per lane the hot state blocks of the active plane set
+// (ctx_count x 16 B; rewritten to 128 when a plane set starts, as every frame
+// is a keyframe) and a line buffer of the row above (the destination is
+// written but never read back).  The CRC table shares the state area: the
+// whole wave checks the CRCs, then primes the states.
 __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
-    __shared__ uint8_t s_tab[512];  // zero[256], one[256]
-    __shared__ uint32_t s_crc[256];
-    __shared__ int16_t s_q[3][256];
-    __shared__ uint32_t s_xp[32];   // x^(8 * 2^j) mod P
-    extern __shared__ __align__(16) uint16_t s_line[];  // [lpw][row_cap]: the row above, per slice
+    extern __shared__ __align__(16) uint8_t smem[];
+    uint8_t *const s_tab = smem;                                     // 512 B
+    int16_t *const s_q = reinterpret_cast<int16_t *>(smem + 512);    // 3 x 256
+    uint32_t *const s_xp = reinterpret_cast<uint32_t *>(smem + 2048);  // x^(8 * 2^j) mod P, j < 32
+    uint8_t *const s_var = smem + kFixedLds;
+    uint32_t *const s_crc = reinterpret_cast<uint32_t *>(s_var);     // 1 KB, before the states
     const int lane = threadIdx.x;
-    for (int i = lane; i < 256; i += blockDim.x) {
+    for (int i = lane; i < 256; i += 64) {
         s_tab[i] = a.tables[i];
         s_tab[256 + i] = a.tables[256 + i];
         s_crc[i] = reinterpret_cast<const uint32_t *>(a.tables + 512)[i];
-        s_q[0][i] = a.quant[i];
-        s_q[1][i] = a.quant[256 + i];
-        s_q[2][i] = a.quant[512 + i];
+        s_q[i] = a.quant[i];
+        s_q[256 + i] = a.quant[256 + i];
+        s_q[512 + i] = a.quant[512 + i];
     }
     if (lane < 32) s_xp[lane] = reinterpret_cast<const uint32_t *>(a.tables + 1536)[lane];
     __syncthreads();
     const int g = blockIdx.x * a.lpw + lane;
+    bool live = lane < a.lpw && g < a.nslices;
+    const uint8_t *sb = nullptr;
+    int64_t n = 0;
+    if (live) {
+        sb = a.pkt + a.soff[g];
+        n = a.slen[g];
+    }
     if (a.ec && !(PP_ABLATE(a.debug) & 2)) {
         // CRC-32 parity of each slice, trailer included, must leave 0.  The
         // whole wave checks one slice at a time: lane t takes the t-th 64th
@@ -209,67 +251,71 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
             for (int o = 32; o >= 1; o >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, o, 64);
             if (lane == j) crc_bad = crc != 0;
         }
-        if (lane < a.lpw && g < a.nslices && crc_bad) {
+        if (live && crc_bad) {
             a.status[g] = 1;
-            return;
+            live = false;
         }
     }
-    if (lane >= a.lpw || g >= a.nslices) return;
+    __syncthreads();
+    const int hot_bytes = a.ctx_count * 16;
+    const int lane_bytes = hot_bytes + a.row_cap * 2;
+    uint8_t *const hot = s_var + lane * lane_bytes;
+    uint16_t *const line = reinterpret_cast<uint16_t *>(hot + hot_bytes);
     const int per = a.nh * a.nv;
-    const int frame = g / per, s = g - frame * per;
-    const uint8_t *const sb = a.pkt + a.soff[g];
-    const int64_t n = a.slen[g];
-    uint16_t *const line = s_line + lane * a.row_cap;
-    // context states of 64 neighbouring slices interleaved by slice (as the
-    // encoder's): context k of slice g at [g / 64][k][g % 64], so a context
-    // that is hot in neighbouring slices -- the same picture content -- shares
-    // their 128-B lines in L2 instead of one line per slice
-    uint8_t *const st0 = a.states + (int64_t)(g >> 6) * (64 * a.state_bytes) + (g & 63) * kCtx;
-    constexpr int kCtxStride = 64 * kCtx;
+    const int frame = live ? g / per : 0, s = live ? g - frame * per : 0;
+    uint8_t *const cold0 = a.cold + (int64_t)(live ? g : 0) * (2 * hot_bytes + 16);
     Dec d;
     {
-        const uintptr_t ap = reinterpret_cast<uintptr_t>(sb);
-        d.w = reinterpret_cast<const uint32_t *>(ap & ~(uintptr_t)3);
-        const int off = (int)(ap & 3);
+        const uintptr_t p = reinterpret_cast<uintptr_t>(sb);
+        d.w = reinterpret_cast<const uint32_t *>(p & ~(uintptr_t)3);
+        const int off = (int)(p & 3);
         d.end = off + (int)n;
         d.range = 0xFF00;
-        d.low = n >= 2 ? ((uint32_t)sb[0] << 8) | sb[1] : 0;
+        d.low = live && n >= 2 ? ((uint32_t)sb[0] << 8) | sb[1] : 0;
         d.pos = off + 2;
         if (d.low >= 0xFF00u) { d.low = 0xFF00u; d.end = d.pos; }
-        d.cur = d.w[d.pos >> 2];
-        d.nxt = d.w[(d.pos >> 2) + 1];
+        d.cur = live ? d.w[d.pos >> 2] : 0u;
+        d.nxt = live ? d.w[(d.pos >> 2) + 1] : 0u;
     }
     uint32_t dummy;
-    if (s == 0 && !dec_rac(d, 128, s_tab, dummy)) {  // keyframe bit
+    if (live && s == 0 && !dec_rac(d, 128, s_tab, dummy)) {  // keyframe bit
         a.status[g] = 2;
-        return;
+        live = false;
     }
     bool bad = false;
-    int hv[9];
-    {
-        uint32_t hb[8];
+    int x0 = 0, x1 = 0, y0 = 0, y1 = 0;
+    if (live) {
+        int hv[9];
+        uint32_t hb[4] = {0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u};
+        // the header's nine symbols share one state block (its cold half
+        // after the slice's two plane sets)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) hb[i] = 0x80808080u;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) hv[i] = dec_symbol<false>(d, hb, s_tab, bad);
-    }
-    const int sx = hv[0], sy = hv[1], sw = hv[2] + 1, sh = hv[3] + 1;
-    if (bad || sx < 0 || sy < 0 || sx > a.nh - sw || sy > a.nv - sh || hv[4] || hv[5] || hv[6] != 3) {
-        a.status[g] = 2;
-        return;
-    }
-    const int x0 = (int)((int64_t)sx * a.w / a.nh), x1 = (int)((int64_t)(sx + sw) * a.w / a.nh);
-    const int y0 = (int)((int64_t)sy * a.h / a.nv), y1 = (int)((int64_t)(sy + sh) * a.h / a.nv);
-    if (x1 - x0 > a.row_cap) {  // wider than this grid's slices
-        a.status[g] = 2;
-        return;
+        for (int i = 0; i < 9; ++i) hv[i] = dec_symbol<false>(d, hb, cold0 + 2 * hot_bytes, s_tab, bad);
+        const int sx = hv[0], sy = hv[1], sw = hv[2] + 1, sh = hv[3] + 1;
+        if (bad || sx < 0 || sy < 0 || sx > a.nh - sw || sy > a.nv - sh || hv[4] || hv[5] || hv[6] != 3) {
+            a.status[g] = 2;
+            live = false;
+        } else {
+            x0 = (int)((int64_t)sx * a.w / a.nh); x1 = (int)((int64_t)(sx + sw) * a.w / a.nh);
+            y0 = (int)((int64_t)sy * a.h / a.nv); y1 = (int)((int64_t)(sy + sh) * a.h / a.nv);
+            if (x1 - x0 > a.row_cap) {  // a slice wider than the grid's: not this record's layout
+                a.status[g] = 2;
+                live = false;
+            }
+        }
     }
     const int mask = (1 << a.bits) - 1;
-    int cur_key = -1;
-    uint32_t blk[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) blk[i] = 0u;
+    if (PP_ABLATE(a.debug) & 1) live = false;
     for (int p = 0; p < 3; p++) {
+        if (p < 2) {  // a plane set starts: its hot states at 128 (the whole wave, converged here)
+            __syncthreads();
+            for (int j = 0; j < a.lpw; ++j) {
+                uint4 *const hs = reinterpret_cast<uint4 *>(s_var + j * lane_bytes);
+                for (int i = lane; i < a.ctx_count; i += 64) hs[i] = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+            }
+            __syncthreads();
+        }
+        if (!live) continue;
         const int pw = p ? ((x1 - x0) + (1 << a.hsub) - 1) >> a.hsub : x1 - x0;
         const int ph = p ? ((y1 - y0) + (1 << a.vsub) - 1) >> a.vsub : y1 - y0;
         const int px0 = p ? x0 >> a.hsub : x0, py0 = p ? y0 >> a.vsub : y0;
@@ -277,30 +323,27 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
         const int64_t ls = p == 0 ? a.ls[0] : p == 1 ? a.ls[1] : a.ls[2];
         const int64_t fs = p == 0 ? a.fs[0] : p == 1 ? a.fs[1] : a.fs[2];
         uint8_t *base = dp + frame * fs + (int64_t)py0 * ls + (int64_t)px0 * a.bytes;
-        const int key0 = p ? a.ctx_count : 0;
+        uint8_t *const cold = cold0 + (p ? hot_bytes : 0);
         int T0prev = 0;  // the row above's first sample, one row later: TL at a row start
         for (int y = 0; y < ph; y++) {
             uint8_t *row = base + (int64_t)y * ls;
-            // `line` holds the row above (never read for the first row); sample
-            // x overwrites line[x] once it is no longer needed as T / TR
+            // `line` holds the row above (zeros above the first row); sample x
+            // overwrites line[x] once T at x + 1 no longer needs it
             int T = y > 0 ? line[0] : 0;
             int TL = y > 1 ? T0prev : 0;
             T0prev = T;
             int L = T;
-            // the row above two columns ahead, read a sample early
             int TR = pw > 1 ? (y > 0 ? line[1] : 0) : T;
             for (int x = 0; x < pw; x++) {
                 const int nTR = x + 2 < pw ? (y > 0 ? line[x + 2] : 0) : TR;
-                int ctx = s_q[0][(L - TL) & 0xFF] + s_q[1][(TL - T) & 0xFF] + s_q[2][(T - TR) & 0xFF];
+                int ctx = s_q[(L - TL) & 0xFF] + s_q[256 + ((TL - T) & 0xFF)] + s_q[512 + ((T - TR) & 0xFF)];
                 const bool neg = ctx < 0;
                 if (neg) ctx = -ctx;
-                const int key = key0 + ctx;
-                if (key != cur_key) {
-                    if (cur_key >= 0 && !(PP_ABLATE(a.debug) & 16)) dblk_store(st0 + cur_key * kCtxStride, blk);
-                    if (!(PP_ABLATE(a.debug) & 8)) dblk_load(blk, st0 + key * kCtxStride);
-                    cur_key = key;
-                }
-                int diff = dec_symbol<true>(d, blk, s_tab, bad);
+                uint4 *const hp = reinterpret_cast<uint4 *>(hot + ctx * 16);
+                const uint4 hx = *hp;
+                uint32_t hb[4] = {hx.x, hx.y, hx.z, hx.w};
+                int diff = dec_symbol<true>(d, hb, cold + ctx * 16, s_tab, bad);
+                *hp = make_uint4(hb[0], hb[1], hb[2], hb[3]);
                 if (neg) diff = -diff;
                 const int v = (dmedian3(L, L + T - TL, T) + diff) & mask;
                 if (a.bytes == 2)
@@ -315,6 +358,7 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
             }
         }
     }
+    if (!live) return;
     (void)dec_rac(d, 129, s_tab, dummy);  // the closing bit at state 129
     a.status[g] = bad ? 2 : ((d.end - d.pos) - 2 - 5 * (a.ec != 0)) != 0 ? 3 : 0;
 }
@@ -329,9 +373,11 @@ struct pp_ffv1_dec {
     int16_t quant[3][256];
     uint8_t *pkt = nullptr, *states = nullptr, *tables = nullptr;
     int64_t pkt_cap = 0, *soff = nullptr, *slen = nullptr;
-    int row_cap = 0;  // widest slice row, rounded to 8 samples
+    int lpw = 1, row_cap = 0;
+    size_t lds = 0;
     int *status = nullptr;
     int16_t *dquant = nullptr;
+    size_t cold_bytes() const { return (size_t)(2 * ctx_count + 1) * 16; }  // per slice
 };
 
 extern "C" int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extra, int extra_size, int w, int h,
@@ -352,14 +398,22 @@ extern "C" int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extra, int ext
         return PP_OK;
     }
     const int64_t ns = (int64_t)D->nh * D->nv * max_frames;
+    // LDS per lane: the hot state blocks of one plane set + the row-above line
+    // buffer (widest slice row, in 16-bit samples, rounded to 8)
     int wmax = 0;
     for (int i = 0; i < D->nh; ++i)
         wmax = std::max(wmax, (int)((int64_t)(i + 1) * w / D->nh - (int64_t)i * w / D->nh));
     D->row_cap = (wmax + 7) / 8 * 8;
-    if ((size_t)D->row_cap * 2 * 64 > kLineLds)
-        PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 decoder: %d-sample slice rows exceed the LDS line buffers", wmax);
+    const size_t lane_bytes = (size_t)D->ctx_count * 16 + (size_t)D->row_cap * 2;
+    int lpw = 1;  // slices per workgroup (PIXPATH_FFV1_DLPW: ablation build only)
+    if (const char *e = PP_KNOB("PIXPATH_FFV1_DLPW")) lpw = std::max(1, std::min(64, std::atoi(e)));
+    D->lpw = std::max(1, std::min(lpw, (int)((kLdsBytes - kFixedLds) / lane_bytes)));
+    D->lds = kFixedLds + std::max<size_t>(1024, D->lpw * lane_bytes);
+    if (D->lds > kLdsBytes)
+        PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 decoder: %d contexts x %d-sample slice rows need %zu B of LDS", D->ctx_count,
+                wmax, D->lds);
     PP_HIP(hipSetDevice(ctx->device));
-    PP_HIP(hipMalloc(&D->states, (size_t)(2 * (int64_t)D->ctx_count * kCtx) * ((ns + 63) / 64 * 64)));
+    PP_HIP(hipMalloc(&D->states, D->cold_bytes() * ns));
     PP_HIP(hipMalloc(&D->soff, sizeof(int64_t) * ns));
     PP_HIP(hipMalloc(&D->slen, sizeof(int64_t) * ns));
     PP_HIP(hipMalloc(&D->status, sizeof(int) * ns));
@@ -434,8 +488,7 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     PP_HIP(hipMemcpyAsync(D->pkt, packets, base, hipMemcpyHostToDevice, st));
     PP_HIP(hipMemcpyAsync(D->soff, soff.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
     PP_HIP(hipMemcpyAsync(D->slen, slen.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
-    const int64_t sb = 2 * (int64_t)D->ctx_count * kCtx;
-    PP_HIP(hipMemsetAsync(D->states, 128, (size_t)sb * ((ns + 63) / 64 * 64), st));
+    PP_HIP(hipMemsetAsync(D->states, 128, D->cold_bytes() * ns, st));
     Ffv1DecArgs a{};
     a.pkt = D->pkt; a.soff = D->soff; a.slen = D->slen;
     for (int p = 0; p < 3; ++p) {
@@ -445,17 +498,15 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     }
     a.w = D->w; a.h = D->h; a.bytes = D->bits > 8 ? 2 : 1; a.bits = D->bits; a.hsub = D->hsub; a.vsub = D->vsub;
     a.nh = D->nh; a.nv = D->nv; a.nslices = ns; a.ec = D->ec;
-    a.ctx_count = D->ctx_count; a.state_bytes = sb;
-    a.states = D->states; a.status = D->status; a.tables = D->tables; a.quant = D->dquant;
-    a.lpw = ffv1_lanes_per_wave(16);
+    a.ctx_count = D->ctx_count; a.row_cap = D->row_cap;
+    a.cold = D->states; a.status = D->status; a.tables = D->tables; a.quant = D->dquant;
+    a.lpw = D->lpw;
     if (const char *e = PP_KNOB("PIXPATH_FFV1_DEBUG")) a.debug = std::atoi(e);
-    a.row_cap = D->row_cap;
     static const hipError_t attr =
         hipFuncSetAttribute(reinterpret_cast<const void *>(ffv1_decode_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLineLds);
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
     PP_HIP(attr);
-    hipLaunchKernelGGL(ffv1_decode_kernel, dim3((ns + a.lpw - 1) / a.lpw), dim3(64),
-                       (size_t)a.lpw * D->row_cap * 2, st, a);
+    hipLaunchKernelGGL(ffv1_decode_kernel, dim3((ns + a.lpw - 1) / a.lpw), dim3(64), D->lds, st, a);
     PP_HIP(hipGetLastError());
     std::vector<int> status(ns);
     PP_HIP(hipMemcpyAsync(status.data(), D->status, sizeof(int) * ns, hipMemcpyDeviceToHost, st));
