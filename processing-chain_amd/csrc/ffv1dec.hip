@@ -43,8 +43,9 @@ struct Ffv1DecArgs {
     int row_cap;                 // samples per lane in the LDS line buffer (>= widest slice row)
     int debug;                   // PIXPATH_FFV1_DEBUG (timing ablation only; the output is wrong):
                                  // 2 no CRC check, 8 no state-block loads, 16 no state-block stores
-    int64_t state_bytes;         // per slice: 2 * ctx_count * 32
-    uint8_t *states;             // [nslices / 64][2 * ctx_count][64][32], primed to 128
+    int64_t state_bytes;         // per slice and half: 2 * ctx_count * 16
+    uint8_t *states;             // hot halves [nslices / 64][2 * ctx_count][64][16], primed to 128
+    uint8_t *cold;               // cold halves, same layout
     int *status;
     const uint8_t *tables;       // zero[256], one[256], crc table
     const int16_t *quant;        // [3][256] (scaled)
@@ -146,13 +147,95 @@ __device__ __forceinline__ int dec_symbol(Dec &d, uint32_t (&b)[8], const uint8_
     return z ? 0 : (neg ? -a : a);
 }
 
-__device__ __forceinline__ void dblk_load(uint32_t (&b)[8], const uint8_t *p) {
-    const uint4 x = reinterpret_cast<const uint4 *>(p)[0], y = reinterpret_cast<const uint4 *>(p)[1];
-    b[0] = x.x; b[1] = x.y; b[2] = x.z; b[3] = x.w; b[4] = y.x; b[5] = y.y; b[6] = y.z; b[7] = y.w;
+// A context's 32 state bytes split in two 16-byte halves.  HOT (the block
+// loaded on every context switch): [0] zero flag, [1..5] exponent
+// bits 0..4, [6..10] sign for e = 0..4, [11..14] mantissa bits 0..3 -- every
+// state a residual below 32 in magnitude touches.  COLD (its own array):
+// [0..4] exponent bits 5..9, [5..9] sign for e = 5..9, [10..14] mantissa bits
+// 4..8, loaded only once a symbol's exponent reaches 5.
+__device__ __forceinline__ uint32_t bget(const uint32_t (&b)[4], int k) { return (b[k >> 2] >> ((k & 3) * 8)) & 0xFFu; }
+__device__ __forceinline__ void bput(uint32_t (&b)[4], int k, uint32_t v) {
+    b[k >> 2] = (b[k >> 2] & ~(0xFFu << ((k & 3) * 8))) | (v << ((k & 3) * 8));
 }
-__device__ __forceinline__ void dblk_store(uint8_t *p, const uint32_t (&b)[8]) {
-    reinterpret_cast<uint4 *>(p)[0] = make_uint4(b[0], b[1], b[2], b[3]);
-    reinterpret_cast<uint4 *>(p)[1] = make_uint4(b[4], b[5], b[6], b[7]);
+
+// get_symbol (ffv1dec.c) for samples of <= 10 bits: exponent e <= 9, so every
+// state index is used at most once per symbol; e >= 10 (not a <= 10-bit
+// stream) sets `bad`.  Decisions read the block as loaded and write the next
+// states into a copy, so no decision waits on the previous one's state-table
+// lookup (neighbouring state bytes share a dword).
+template <bool SIGNED>
+__device__ __forceinline__ int dec_symbol_split(Dec &d, uint32_t (&h)[4], uint8_t *cold, const uint8_t *tab, bool &bad) {
+    const uint32_t h0[4] = {h[0], h[1], h[2], h[3]};
+    uint32_t ns;
+    const uint32_t z = dec_rac(d, bget(h0, 0), tab, ns);
+    bput(h, 0, ns);
+    if (z) return 0;
+    int e = 0, a = 1;
+    bool go = true;
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+        if (go) {
+            const uint32_t bit = dec_rac(d, bget(h0, 1 + i), tab, ns);
+            bput(h, 1 + i, ns);
+            if (bit) e = i + 1;
+            else go = false;
+        }
+    uint32_t neg;
+    if (go) {  // e >= 5: the cold half
+        const uint4 x = *reinterpret_cast<const uint4 *>(cold);
+        const uint32_t c0[4] = {x.x, x.y, x.z, x.w};
+        uint32_t c[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int i = 5; i < 10; ++i)
+            if (go) {
+                const uint32_t bit = dec_rac(d, bget(c0, i - 5), tab, ns);
+                bput(c, i - 5, ns);
+                if (bit) e = i + 1;
+                else go = false;
+            }
+        if (go) bad = true;
+#pragma unroll
+        for (int i = 8; i >= 4; --i)
+            if (i < e) {
+                a = 2 * a + (int)dec_rac(d, bget(c0, 10 + i - 4), tab, ns);
+                bput(c, 10 + i - 4, ns);
+            }
+#pragma unroll
+        for (int i = 3; i >= 0; --i) {
+            a = 2 * a + (int)dec_rac(d, bget(h0, 11 + i), tab, ns);
+            bput(h, 11 + i, ns);
+        }
+        neg = 0;
+        if constexpr (SIGNED) {
+            const int k = min(e, 9);  // sign state 5 + (k - 5) of the cold half
+            const uint32_t sv = k == 5 ? bget(c0, 5) : k == 6 ? bget(c0, 6) : k == 7 ? bget(c0, 7) : k == 8 ? bget(c0, 8) : bget(c0, 9);
+            neg = dec_rac(d, sv, tab, ns);
+            if (k == 5) bput(c, 5, ns);
+            else if (k == 6) bput(c, 6, ns);
+            else if (k == 7) bput(c, 7, ns);
+            else if (k == 8) bput(c, 8, ns);
+            else bput(c, 9, ns);
+        }
+        *reinterpret_cast<uint4 *>(cold) = make_uint4(c[0], c[1], c[2], c[3]);
+    } else {
+#pragma unroll
+        for (int i = 3; i >= 0; --i)
+            if (i < e) {
+                a = 2 * a + (int)dec_rac(d, bget(h0, 11 + i), tab, ns);
+                bput(h, 11 + i, ns);
+            }
+        neg = 0;
+        if constexpr (SIGNED) {  // sign state 6 + e, e in 0..4
+            const uint32_t sv = e == 0 ? bget(h0, 6) : e == 1 ? bget(h0, 7) : e == 2 ? bget(h0, 8) : e == 3 ? bget(h0, 9) : bget(h0, 10);
+            neg = dec_rac(d, sv, tab, ns);
+            if (e == 0) bput(h, 6, ns);
+            else if (e == 1) bput(h, 7, ns);
+            else if (e == 2) bput(h, 8, ns);
+            else if (e == 3) bput(h, 9, ns);
+            else bput(h, 10, ns);
+        }
+    }
+    return neg ? -a : a;
 }
 
 // a(x) b(x) mod P for the slice CRC's polynomial (CRC-32 IEEE, MSB first)
@@ -165,6 +248,16 @@ __device__ __forceinline__ uint32_t gf2_mulmod(uint32_t a, uint32_t b) {
     }
     return r;
 }
+
+__device__ __forceinline__ void dblk_load(uint32_t (&b)[8], const uint8_t *p) {
+    const uint4 x = reinterpret_cast<const uint4 *>(p)[0], y = reinterpret_cast<const uint4 *>(p)[1];
+    b[0] = x.x; b[1] = x.y; b[2] = x.z; b[3] = x.w; b[4] = y.x; b[5] = y.y; b[6] = y.z; b[7] = y.w;
+}
+__device__ __forceinline__ void dblk_store(uint8_t *p, const uint32_t (&b)[8]) {
+    reinterpret_cast<uint4 *>(p)[0] = make_uint4(b[0], b[1], b[2], b[3]);
+    reinterpret_cast<uint4 *>(p)[1] = make_uint4(b[4], b[5], b[6], b[7]);
+}
+
 
 __device__ __forceinline__ int dmedian3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 
@@ -224,8 +317,9 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
     // encoder's): context k of slice g at [g / 64][k][g % 64], so a context
     // that is hot in neighbouring slices -- the same picture content -- shares
     // their 128-B lines in L2 instead of one line per slice
-    uint8_t *const st0 = a.states + (int64_t)(g >> 6) * (64 * a.state_bytes) + (g & 63) * kCtx;
-    constexpr int kCtxStride = 64 * kCtx;
+    uint8_t *const st0 = a.states + (int64_t)(g >> 6) * (64 * a.state_bytes) + (g & 63) * 16;
+    uint8_t *const co0 = a.cold + (int64_t)(g >> 6) * (64 * a.state_bytes) + (g & 63) * 16;
+    constexpr int kCtxStride = 64 * 16;
     Dec d;
     {
         const uintptr_t ap = reinterpret_cast<uintptr_t>(sb);
@@ -266,9 +360,7 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
     }
     const int mask = (1 << a.bits) - 1;
     int cur_key = -1;
-    uint32_t blk[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) blk[i] = 0u;
+    uint32_t blk[4] = {0u, 0u, 0u, 0u};
     for (int p = 0; p < 3; p++) {
         const int pw = p ? ((x1 - x0) + (1 << a.hsub) - 1) >> a.hsub : x1 - x0;
         const int ph = p ? ((y1 - y0) + (1 << a.vsub) - 1) >> a.vsub : y1 - y0;
@@ -296,11 +388,15 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
                 if (neg) ctx = -ctx;
                 const int key = key0 + ctx;
                 if (key != cur_key) {
-                    if (cur_key >= 0 && !(PP_ABLATE(a.debug) & 16)) dblk_store(st0 + cur_key * kCtxStride, blk);
-                    if (!(PP_ABLATE(a.debug) & 8)) dblk_load(blk, st0 + key * kCtxStride);
+                    if (cur_key >= 0 && !(PP_ABLATE(a.debug) & 16))
+                        *reinterpret_cast<uint4 *>(st0 + cur_key * kCtxStride) = make_uint4(blk[0], blk[1], blk[2], blk[3]);
+                    if (!(PP_ABLATE(a.debug) & 8)) {
+                        const uint4 x = *reinterpret_cast<const uint4 *>(st0 + key * kCtxStride);
+                        blk[0] = x.x; blk[1] = x.y; blk[2] = x.z; blk[3] = x.w;
+                    }
                     cur_key = key;
                 }
-                int diff = dec_symbol<true>(d, blk, s_tab, bad);
+                int diff = dec_symbol_split<true>(d, blk, co0 + cur_key * kCtxStride, s_tab, bad);
                 if (neg) diff = -diff;
                 const int v = (dmedian3(L, L + T - TL, T) + diff) & mask;
                 if (a.bytes == 2)
@@ -359,7 +455,7 @@ extern "C" int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extra, int ext
     if ((size_t)D->row_cap * 2 * 64 > kLineLds)
         PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 decoder: %d-sample slice rows exceed the LDS line buffers", wmax);
     PP_HIP(hipSetDevice(ctx->device));
-    PP_HIP(hipMalloc(&D->states, (size_t)(2 * (int64_t)D->ctx_count * kCtx) * ((ns + 63) / 64 * 64)));
+    PP_HIP(hipMalloc(&D->states, (size_t)(2 * (int64_t)D->ctx_count * kCtx) * ((ns + 63) / 64 * 64)));  // both halves
     PP_HIP(hipMalloc(&D->soff, sizeof(int64_t) * ns));
     PP_HIP(hipMalloc(&D->slen, sizeof(int64_t) * ns));
     PP_HIP(hipMalloc(&D->status, sizeof(int) * ns));
@@ -434,8 +530,9 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     PP_HIP(hipMemcpyAsync(D->pkt, packets, base, hipMemcpyHostToDevice, st));
     PP_HIP(hipMemcpyAsync(D->soff, soff.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
     PP_HIP(hipMemcpyAsync(D->slen, slen.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
-    const int64_t sb = 2 * (int64_t)D->ctx_count * kCtx;
-    PP_HIP(hipMemsetAsync(D->states, 128, (size_t)sb * ((ns + 63) / 64 * 64), st));
+    const int64_t sb = 2 * (int64_t)D->ctx_count * 16;  // one half, per slice
+    const size_t half = (size_t)sb * ((ns + 63) / 64 * 64);
+    PP_HIP(hipMemsetAsync(D->states, 128, 2 * half, st));
     Ffv1DecArgs a{};
     a.pkt = D->pkt; a.soff = D->soff; a.slen = D->slen;
     for (int p = 0; p < 3; ++p) {
@@ -446,7 +543,7 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     a.w = D->w; a.h = D->h; a.bytes = D->bits > 8 ? 2 : 1; a.bits = D->bits; a.hsub = D->hsub; a.vsub = D->vsub;
     a.nh = D->nh; a.nv = D->nv; a.nslices = ns; a.ec = D->ec;
     a.ctx_count = D->ctx_count; a.state_bytes = sb;
-    a.states = D->states; a.status = D->status; a.tables = D->tables; a.quant = D->dquant;
+    a.states = D->states; a.cold = D->states + half; a.status = D->status; a.tables = D->tables; a.quant = D->dquant;
     a.lpw = ffv1_lanes_per_wave(16);
     if (const char *e = PP_KNOB("PIXPATH_FFV1_DEBUG")) a.debug = std::atoi(e);
     a.row_cap = D->row_cap;

@@ -9,9 +9,9 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 tail -2 gpurun_out/ffv1_tests_$TAG.log
 timeout -k 10 120 python -u tools/ffv1_dec_chunks.py 600 60 | tee gpurun_out/ffv1_dec_$TAG.txt
 . tools/ablate_env.sh
-for l in 8 32; do
-  echo "LPW=$l $(PIXPATH_FFV1_LPW=$l timeout -k 10 120 python -u tools/ffv1_dec_chunks.py 600)" | tee -a gpurun_out/ffv1_dec_$TAG.txt || exit 1
+for l in; do
+  echo "DPF=$l $(PIXPATH_FFV1_DPF=$l timeout -k 10 120 python -u tools/ffv1_dec_chunks.py 600)" | tee -a gpurun_out/ffv1_dec_$TAG.txt || exit 1
 done
-for dbg in 2; do
+for dbg in; do
   echo "DEBUG=$dbg $(PIXPATH_FFV1_DEBUG=$dbg timeout -k 10 120 python -u tools/ffv1_dec_chunks.py 600)" | tee -a gpurun_out/ffv1_dec_$TAG.txt || exit 1
 done
