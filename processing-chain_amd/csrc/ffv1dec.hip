@@ -55,15 +55,24 @@ struct Ffv1DecArgs {
 // state: a symbol's state bytes come from the current context's 32-byte block
 // in 8 VGPRs (all read before its first decision, updated bytes written after
 // the last, so the LDS state-table lookups never sit on the low/range chain).
-// The bytestream is read a dword at a time through a two-word register
-// window, the next word loaded four refills before it is needed, so no refill
-// waits on memory.
+// The bytestream is read a dword at a time: `cur` holds the word at `pos`,
+// and each sample issues the load of the following word into `nxt` before its
+// state-block load (dec_prefetch), so a refill that enters that word takes it
+// from a register whose load has completed with the block's.  A refill that
+// enters any other word loads it there (the header, or a sample past two
+// words).
 struct Dec {
     uint32_t low, range;
     int pos, end;  // byte positions relative to the dword-aligned base `w`
     uint32_t cur, nxt;
+    int nk;        // word index held in `nxt`
     const uint32_t *w;
 };
+
+__device__ __forceinline__ void dec_prefetch(Dec &d) {
+    d.nk = (d.pos >> 2) + 1;
+    d.nxt = d.w[d.nk];
+}
 
 __device__ __forceinline__ void dec_refill(Dec &d) {
     if (d.range < 0x100u) {
@@ -73,8 +82,8 @@ __device__ __forceinline__ void dec_refill(Dec &d) {
             d.low += (d.cur >> ((d.pos & 3) * 8)) & 0xFFu;
             d.pos++;
             if ((d.pos & 3) == 0) {
-                d.cur = d.nxt;
-                d.nxt = d.w[(d.pos >> 2) + 1];
+                if ((d.pos >> 2) == d.nk) d.cur = d.nxt;
+                else d.cur = d.w[d.pos >> 2];
             }
         }
     }
@@ -322,16 +331,16 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
     constexpr int kCtxStride = 64 * 16;
     Dec d;
     {
-        const uintptr_t ap = reinterpret_cast<uintptr_t>(sb);
-        d.w = reinterpret_cast<const uint32_t *>(ap & ~(uintptr_t)3);
-        const int off = (int)(ap & 3);
+        // pkt is 256-B aligned: the slice's misalignment is its offset's
+        const int off = (int)(a.soff[g] & 3);
+        d.w = reinterpret_cast<const uint32_t *>(sb - off);
         d.end = off + (int)n;
         d.range = 0xFF00;
         d.low = n >= 2 ? ((uint32_t)sb[0] << 8) | sb[1] : 0;
         d.pos = off + 2;
         if (d.low >= 0xFF00u) { d.low = 0xFF00u; d.end = d.pos; }
         d.cur = d.w[d.pos >> 2];
-        d.nxt = d.w[(d.pos >> 2) + 1];
+        dec_prefetch(d);
     }
     uint32_t dummy;
     if (s == 0 && !dec_rac(d, 128, s_tab, dummy)) {  // keyframe bit
@@ -387,6 +396,7 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
                 const bool neg = ctx < 0;
                 if (neg) ctx = -ctx;
                 const int key = key0 + ctx;
+                dec_prefetch(d);
                 if (key != cur_key) {
                     if (cur_key >= 0 && !(PP_ABLATE(a.debug) & 16))
                         *reinterpret_cast<uint4 *>(st0 + cur_key * kCtxStride) = make_uint4(blk[0], blk[1], blk[2], blk[3]);
