@@ -42,7 +42,7 @@ struct Ffv1DecArgs {
     int lpw;                     // slices (active lanes) per 64-lane workgroup: ffv1_lanes_per_wave()
     int row_cap;                 // samples per lane in the LDS line buffer (>= widest slice row)
     int debug;                   // PIXPATH_FFV1_DEBUG (timing ablation only; the output is wrong):
-                                 // 2 no CRC check, 8 no state-block loads, 16 no state-block stores
+                                 // 2 no CRC check
     int64_t state_bytes;         // per slice and half: 2 * ctx_count * 16
     uint8_t *states;             // hot halves [nslices / 64][2 * ctx_count][64][16], primed to 128
     uint8_t *cold;               // cold halves, same layout
@@ -270,6 +270,7 @@ __device__ __forceinline__ void dblk_store(uint8_t *p, const uint32_t (&b)[8]) {
 
 __device__ __forceinline__ int dmedian3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 
+template <int BYTES>
 __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
     __shared__ uint8_t s_tab[512];  // zero[256], one[256]
     __shared__ uint32_t s_crc[256];
@@ -368,8 +369,8 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
         return;
     }
     const int mask = (1 << a.bits) - 1;
-    int cur_key = -1;
-    uint32_t blk[4] = {0u, 0u, 0u, 0u};
+    int cur_key = 0;  // context 0 holding its initial states: the first write-back rewrites 128s
+    uint32_t blk[4] = {0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u};
     for (int p = 0; p < 3; p++) {
         const int pw = p ? ((x1 - x0) + (1 << a.hsub) - 1) >> a.hsub : x1 - x0;
         const int ph = p ? ((y1 - y0) + (1 << a.vsub) - 1) >> a.vsub : y1 - y0;
@@ -377,9 +378,16 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
         uint8_t *dp = p == 0 ? a.dst[0] : p == 1 ? a.dst[1] : a.dst[2];
         const int64_t ls = p == 0 ? a.ls[0] : p == 1 ? a.ls[1] : a.ls[2];
         const int64_t fs = p == 0 ? a.fs[0] : p == 1 ? a.fs[1] : a.fs[2];
-        uint8_t *base = dp + frame * fs + (int64_t)py0 * ls + (int64_t)px0 * a.bytes;
+        uint8_t *base = dp + frame * fs + (int64_t)py0 * ls + (int64_t)px0 * BYTES;
         const int key0 = p ? a.ctx_count : 0;
         int T0prev = 0;  // the row above's first sample, one row later: TL at a row start
+        auto put = [&](uint8_t *r, int xx, int vv) {
+            if (BYTES == 2)
+                reinterpret_cast<uint16_t *>(r)[xx] = (uint16_t)vv;
+            else
+                r[xx] = (uint8_t)vv;
+        };
+        int pv = 0;
         for (int y = 0; y < ph; y++) {
             uint8_t *row = base + (int64_t)y * ls;
             // `line` holds the row above (never read for the first row); sample
@@ -397,28 +405,34 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
                 if (neg) ctx = -ctx;
                 const int key = key0 + ctx;
                 dec_prefetch(d);
-                if (key != cur_key) {
-                    if (cur_key >= 0 && !(PP_ABLATE(a.debug) & 16))
-                        *reinterpret_cast<uint4 *>(st0 + cur_key * kCtxStride) = make_uint4(blk[0], blk[1], blk[2], blk[3]);
-                    if (!(PP_ABLATE(a.debug) & 8)) {
-                        const uint4 x = *reinterpret_cast<const uint4 *>(st0 + key * kCtxStride);
-                        blk[0] = x.x; blk[1] = x.y; blk[2] = x.z; blk[3] = x.w;
-                    }
+                // Branch-free: memory operations complete in issue order, so the
+                // block load goes out before the previous sample's store and the
+                // write-back of the current block, and waiting for it does not
+                // wait for their acks.  Same context: the load is stale and the
+                // registers are kept.
+                {
+                    const uint4 nb = *reinterpret_cast<const uint4 *>(st0 + key * kCtxStride);
+                    // (x = 0: the previous row's last sample lands on row[0] until x = 1 rewrites it)
+                    put(row, max(x - 1, 0), pv);
+                    *reinterpret_cast<uint4 *>(st0 + cur_key * kCtxStride) = make_uint4(blk[0], blk[1], blk[2], blk[3]);
+                    const bool same = key == cur_key;
+                    blk[0] = same ? blk[0] : nb.x;
+                    blk[1] = same ? blk[1] : nb.y;
+                    blk[2] = same ? blk[2] : nb.z;
+                    blk[3] = same ? blk[3] : nb.w;
                     cur_key = key;
                 }
                 int diff = dec_symbol_split<true>(d, blk, co0 + cur_key * kCtxStride, s_tab, bad);
                 if (neg) diff = -diff;
                 const int v = (dmedian3(L, L + T - TL, T) + diff) & mask;
-                if (a.bytes == 2)
-                    reinterpret_cast<uint16_t *>(row)[x] = (uint16_t)v;
-                else
-                    row[x] = (uint8_t)v;
+                pv = v;  // stored during the next sample, after its block load
                 line[x] = (uint16_t)v;
                 TL = T;
                 T = TR;
                 TR = nTR;
                 L = v;
             }
+            if (pw > 0) put(row, pw - 1, pv);
         }
     }
     (void)dec_rac(d, 129, s_tab, dummy);  // the closing bit at state 129
@@ -557,12 +571,20 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     a.lpw = ffv1_lanes_per_wave(16);
     if (const char *e = PP_KNOB("PIXPATH_FFV1_DEBUG")) a.debug = std::atoi(e);
     a.row_cap = D->row_cap;
-    static const hipError_t attr =
-        hipFuncSetAttribute(reinterpret_cast<const void *>(ffv1_decode_kernel),
+    static const hipError_t attr1 =
+        hipFuncSetAttribute(reinterpret_cast<const void *>(ffv1_decode_kernel<1>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLineLds);
-    PP_HIP(attr);
-    hipLaunchKernelGGL(ffv1_decode_kernel, dim3((ns + a.lpw - 1) / a.lpw), dim3(64),
-                       (size_t)a.lpw * D->row_cap * 2, st, a);
+    static const hipError_t attr2 =
+        hipFuncSetAttribute(reinterpret_cast<const void *>(ffv1_decode_kernel<2>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLineLds);
+    PP_HIP(attr1);
+    PP_HIP(attr2);
+    if (a.bytes == 2)
+        hipLaunchKernelGGL(ffv1_decode_kernel<2>, dim3((ns + a.lpw - 1) / a.lpw), dim3(64),
+                           (size_t)a.lpw * D->row_cap * 2, st, a);
+    else
+        hipLaunchKernelGGL(ffv1_decode_kernel<1>, dim3((ns + a.lpw - 1) / a.lpw), dim3(64),
+                           (size_t)a.lpw * D->row_cap * 2, st, a);
     PP_HIP(hipGetLastError());
     std::vector<int> status(ns);
     PP_HIP(hipMemcpyAsync(status.data(), D->status, sizeof(int) * ns, hipMemcpyDeviceToHost, st));
