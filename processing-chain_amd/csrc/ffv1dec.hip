@@ -270,7 +270,16 @@ __device__ __forceinline__ void dblk_store(uint8_t *p, const uint32_t (&b)[8]) {
 
 __device__ __forceinline__ int dmedian3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 
-template <int BYTES>
+// pixpath's own first quantiser (ffv1host.cpp ffv1_quant: min(5, bit length
+// |d|), odd-mirrored, scale 1) as ALU code: the only lookup that depends on
+// the sample just decoded leaves LDS
+__device__ __forceinline__ int dquant0(int d) {  // d already & 0xFF
+    const int m = d < 128 ? d : (d == 128 ? 127 : 256 - d);
+    const int q = min(32 - __clz(m), 5);
+    return d < 128 ? q : -q;
+}
+
+template <int BYTES, bool QALU>
 __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
     __shared__ uint8_t s_tab[512];  // zero[256], one[256]
     __shared__ uint32_t s_crc[256];
@@ -400,7 +409,8 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
             int TR = pw > 1 ? (y > 0 ? line[1] : 0) : T;
             for (int x = 0; x < pw; x++) {
                 const int nTR = x + 2 < pw ? (y > 0 ? line[x + 2] : 0) : TR;
-                int ctx = s_q[0][(L - TL) & 0xFF] + s_q[1][(TL - T) & 0xFF] + s_q[2][(T - TR) & 0xFF];
+                int ctx = (QALU ? dquant0((L - TL) & 0xFF) : s_q[0][(L - TL) & 0xFF]) + s_q[1][(TL - T) & 0xFF] +
+                          s_q[2][(T - TR) & 0xFF];
                 const bool neg = ctx < 0;
                 if (neg) ctx = -ctx;
                 const int key = key0 + ctx;
@@ -450,6 +460,7 @@ struct pp_ffv1_dec {
     uint8_t *pkt = nullptr, *states = nullptr, *tables = nullptr;
     int64_t pkt_cap = 0, *soff = nullptr, *slen = nullptr;
     int row_cap = 0;  // widest slice row, rounded to 8 samples
+    bool q0_alu = false;  // the record's first quantiser is pixpath's (dquant0)
     int *status = nullptr;
     int16_t *dquant = nullptr;
 };
@@ -467,6 +478,8 @@ extern "C" int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extra, int ext
     D->bits = rec.bits; D->hsub = rec.hsub; D->vsub = rec.vsub; D->nh = rec.nh; D->nv = rec.nv; D->ec = rec.ec;
     D->ctx_count = rec.ctx_count;
     std::memcpy(D->quant, rec.quant, sizeof(D->quant));
+    D->q0_alu = true;
+    for (int i = 0; i < 256; ++i) D->q0_alu = D->q0_alu && D->quant[0][i] == ffv1_quant(i);
     if (!ctx) {
         *out = D.release();
         return PP_OK;
@@ -571,20 +584,27 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     a.lpw = ffv1_lanes_per_wave(16);
     if (const char *e = PP_KNOB("PIXPATH_FFV1_DEBUG")) a.debug = std::atoi(e);
     a.row_cap = D->row_cap;
-    static const hipError_t attr1 =
-        hipFuncSetAttribute(reinterpret_cast<const void *>(ffv1_decode_kernel<1>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLineLds);
-    static const hipError_t attr2 =
-        hipFuncSetAttribute(reinterpret_cast<const void *>(ffv1_decode_kernel<2>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLineLds);
-    PP_HIP(attr1);
-    PP_HIP(attr2);
-    if (a.bytes == 2)
-        hipLaunchKernelGGL(ffv1_decode_kernel<2>, dim3((ns + a.lpw - 1) / a.lpw), dim3(64),
-                           (size_t)a.lpw * D->row_cap * 2, st, a);
+    static const hipError_t attr = [] {
+        const void *fns[4] = {reinterpret_cast<const void *>(ffv1_decode_kernel<1, false>),
+                              reinterpret_cast<const void *>(ffv1_decode_kernel<1, true>),
+                              reinterpret_cast<const void *>(ffv1_decode_kernel<2, false>),
+                              reinterpret_cast<const void *>(ffv1_decode_kernel<2, true>)};
+        for (const void *f : fns)
+            if (hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLineLds))
+                return e;
+        return hipSuccess;
+    }();
+    PP_HIP(attr);
+    const dim3 grid((ns + a.lpw - 1) / a.lpw), block(64);
+    const size_t lds = (size_t)a.lpw * D->row_cap * 2;
+    if (a.bytes == 2 && D->q0_alu)
+        hipLaunchKernelGGL((ffv1_decode_kernel<2, true>), grid, block, lds, st, a);
+    else if (a.bytes == 2)
+        hipLaunchKernelGGL((ffv1_decode_kernel<2, false>), grid, block, lds, st, a);
+    else if (D->q0_alu)
+        hipLaunchKernelGGL((ffv1_decode_kernel<1, true>), grid, block, lds, st, a);
     else
-        hipLaunchKernelGGL(ffv1_decode_kernel<1>, dim3((ns + a.lpw - 1) / a.lpw), dim3(64),
-                           (size_t)a.lpw * D->row_cap * 2, st, a);
+        hipLaunchKernelGGL((ffv1_decode_kernel<1, false>), grid, block, lds, st, a);
     PP_HIP(hipGetLastError());
     std::vector<int> status(ns);
     PP_HIP(hipMemcpyAsync(status.data(), D->status, sizeof(int) * ns, hipMemcpyDeviceToHost, st));
