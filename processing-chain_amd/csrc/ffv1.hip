@@ -404,6 +404,94 @@ __device__ __forceinline__ void enc_symbol(Enc &c, uint32_t (&b)[8], int v, cons
     if (SIGNED && E >= 0) sput_dyn(b, 11 + (e < 0 ? 0 : e), nsg, nz);
 }
 
+// A context's 32 state bytes split in two 16-byte halves (the decoder's
+// layout, ffv1dec.hip).  HOT, the block the coder forwards and prefetches:
+// [0] zero flag, [1..5] exponent bits 0..4, [6..10] sign for e = 0..4,
+// [11..14] mantissa bits 0..3 -- every state a residual below 32 touches.
+// COLD, read and written in place only while the wave's longest exponent is
+// >= 5: [0..4] exponent bits 5..9, [5..9] sign for e = 5..9, [10..14]
+// mantissa bits 4..8.
+__device__ __forceinline__ uint32_t hget(const uint32_t (&b)[4], int k) { return (b[k >> 2] >> ((k & 3) * 8)) & 0xFFu; }
+__device__ __forceinline__ void hput(uint32_t (&b)[4], int k, uint32_t v) {
+    b[k >> 2] = (b[k >> 2] & ~(0xFFu << ((k & 3) * 8))) | (v << ((k & 3) * 8));
+}
+// enc_symbol on the split block: the same decisions in the same order
+template <bool SIGNED>
+__device__ __forceinline__ void enc_symbol_split(Enc &c, uint32_t (&b)[4], uint8_t *cold, int v, const uint8_t *tab) {
+    const uint32_t a = (uint32_t)(v < 0 ? -v : v);
+    const bool nz = v != 0;
+    const int e = nz ? 31 - __clz(a) : -1;
+    const int E = wave_max_e(e);
+    uint32_t cb[4] = {0u, 0u, 0u, 0u};
+    if (E >= 5) {  // wave-uniform
+        const uint4 x = *reinterpret_cast<const uint4 *>(cold);
+        cb[0] = x.x; cb[1] = x.y; cb[2] = x.z; cb[3] = x.w;
+    }
+    const uint32_t s0 = hget(b, 0);
+    uint32_t su[10], sm[9], ss = 0, n0, nu[10], nm[9], nsg = 0;
+    n0 = tab[s0 | (nz ? 0u : 256u)];
+#pragma unroll
+    for (int i = 0; i < 10; ++i)
+        if (i <= E) {
+            su[i] = i < 5 ? hget(b, 1 + i) : hget(cb, i - 5);
+            nu[i] = tab[su[i] | (i < e ? 256u : 0u)];
+        }
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+        if (i < E) {
+            sm[i] = i < 4 ? hget(b, 11 + i) : hget(cb, 10 + i - 4);
+            nm[i] = tab[sm[i] | (((a >> i) & 1u) << 8)];
+        }
+    const int es = e < 0 ? 0 : e;
+    if (SIGNED && E >= 0) {  // sign state of exponent es: compile-time byte indices under selects
+#pragma unroll
+        for (int i = 0; i < 10; ++i) ss = es == i ? (i < 5 ? hget(b, 6 + i) : hget(cb, i)) : ss;
+        nsg = tab[ss | (v < 0 ? 256u : 0u)];
+    }
+    enc_dec(c, s0, !nz);
+#pragma unroll
+    for (int i = 0; i < 10; ++i)
+        if (i <= E) enc_dec(c, i <= e ? su[i] : 0u, i < e);
+#pragma unroll
+    for (int i = 8; i >= 0; --i)
+        if (i < E) enc_dec(c, i < e ? sm[i] : 0u, i < e && ((a >> i) & 1u));
+    if (SIGNED && E >= 0) enc_dec(c, nz ? ss : 0u, v < 0);
+    hput(b, 0, n0);
+#pragma unroll
+    for (int i = 0; i < 10; ++i)
+        if (i <= E) {
+            if (i < 5) hput(b, 1 + i, i <= e ? nu[i] : su[i]);
+            else hput(cb, i - 5, i <= e ? nu[i] : su[i]);
+        }
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+        if (i < E) {
+            if (i < 4) hput(b, 11 + i, i < e ? nm[i] : sm[i]);
+            else hput(cb, 10 + i - 4, i < e ? nm[i] : sm[i]);
+        }
+    if (SIGNED && E >= 0) {
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            const bool on = nz && es == i;
+            if (i < 5) hput(b, 6 + i, on ? nsg : hget(b, 6 + i));
+            else hput(cb, i, on ? nsg : hget(cb, i));
+        }
+    }
+    if (E >= 5) *reinterpret_cast<uint4 *>(cold) = make_uint4(cb[0], cb[1], cb[2], cb[3]);
+}
+
+__device__ __forceinline__ void hblk_load(uint32_t (&b)[4], const uint8_t *p) {
+    const uint4 x = *reinterpret_cast<const uint4 *>(p);
+    b[0] = x.x; b[1] = x.y; b[2] = x.z; b[3] = x.w;
+}
+__device__ __forceinline__ void hblk_store(uint8_t *p, const uint32_t (&b)[4]) {
+    *reinterpret_cast<uint4 *>(p) = make_uint4(b[0], b[1], b[2], b[3]);
+}
+__device__ __forceinline__ void hblk_sel(uint32_t (&d)[4], bool c, const uint32_t (&x)[4], const uint32_t (&y)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d[i] = c ? x[i] : y[i];
+}
+
 __device__ __forceinline__ void blk_load(uint32_t (&b)[8], const uint8_t *p) {
     const uint4 x = reinterpret_cast<const uint4 *>(p)[0], y = reinterpret_cast<const uint4 *>(p)[1];
     b[0] = x.x; b[1] = x.y; b[2] = x.z; b[3] = x.w; b[4] = y.x; b[5] = y.y; b[6] = y.z; b[7] = y.w;
@@ -431,11 +519,13 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
     if (g >= a.nslices) return;
     const SliceGeo q = slice_geo(g, a.w, a.h, a.nh, a.nv, a.hsub, a.vsub);
     const int len = q.len();
-    // context states of the 64-slice group interleaved by slice: context k of
-    // slice g at [g / 64][k][g % 64] -- a 128-B line holds one context of 4
-    // slices (a context that is hot in one slice is hot in its neighbours)
-    uint8_t *const st0 = a.states + (int64_t)(g >> 6) * (64 * kStateBytes) + (g & 63) * kCtxSize;
-    constexpr int kCtxStride = 64 * kCtxSize;
+    // context states of the 64-slice group interleaved by slice, hot halves
+    // then cold halves: context k of slice g at [g / 64][half][k][g % 64][16]
+    // -- a 128-B line holds one context's half of 8 slices (a context that is
+    // hot in one slice is hot in its neighbours)
+    uint8_t *const st0 = a.states + (int64_t)(g >> 6) * (64 * kStateBytes) + (g & 63) * 16;
+    uint8_t *const co0 = st0 + 64 * kStateBytes / 2;
+    constexpr int kCtxStride = 64 * 16;
     // tokens of slice g: group g / 64 of the modelling layout, lane g % 64
     const uint32_t *tp = a.tok + (int64_t)(g >> 6) * a.tok_len * 64 + (g & 63);
     Enc c;
@@ -490,31 +580,31 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
     // through register copies at the loop latch and waits there.)
     uint32_t tk[4] = {tok(0), tok(1), tok(2), tok(3)};
     int km2 = -1, km1 = -1;
-    uint32_t cur[8], prev[8], pre[2][8];
+    uint32_t cur[4], prev[4], pre[2][4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) cur[i] = prev[i] = 0u;
-    blk_load(pre[0], st0 + (tk[0] >> 16) * kCtxStride);
-    blk_load(pre[1], st0 + (tk[1] >> 16) * kCtxStride);
+    for (int i = 0; i < 4; ++i) cur[i] = prev[i] = 0u;
+    hblk_load(pre[0], st0 + (tk[0] >> 16) * kCtxStride);
+    hblk_load(pre[1], st0 + (tk[1] >> 16) * kCtxStride);
     auto step = [&](int i, auto ph_c) {
         constexpr int PH = decltype(ph_c)::value;
         const uint32_t t0 = tk[PH], t2 = tk[(PH + 2) & 3];
         const int k0 = (int)(t0 >> 16);
         const int v = (int)(int16_t)(t0 & 0xFFFFu);
-        uint32_t b[8];
-        // block of this sample: the previous sample's, the one before, or the prefetched
+        uint32_t b[4];
+        // hot block of this sample: the previous sample's, the one before, or the prefetched
         {
-            uint32_t tmp[8];
-            blk_sel(tmp, k0 == km2, prev, pre[PH & 1]);
-            blk_sel(b, k0 == km1, cur, tmp);
+            uint32_t tmp[4];
+            hblk_sel(tmp, k0 == km2, prev, pre[PH & 1]);
+            hblk_sel(b, k0 == km1, cur, tmp);
         }
-        // the block of sample i + 2 (used unless sample i or i + 1 forwards it)
-        if (!(PP_ABLATE(a.debug) & 1)) blk_load(pre[PH & 1], st0 + (t2 >> 16) * kCtxStride);
+        // the hot block of sample i + 2 (used unless sample i or i + 1 forwards it)
+        if (!(PP_ABLATE(a.debug) & 1)) hblk_load(pre[PH & 1], st0 + (t2 >> 16) * kCtxStride);
         tk[PH] = tok(i + 4);
-        enc_symbol<true>(c, b, v, s_tab);
-        if (!(PP_ABLATE(a.debug) & 2)) blk_store(st0 + k0 * kCtxStride, b);
+        enc_symbol_split<true>(c, b, co0 + k0 * kCtxStride, v, s_tab);
+        if (!(PP_ABLATE(a.debug) & 2)) hblk_store(st0 + k0 * kCtxStride, b);
         if (PH == 3 && !(PP_ABLATE(a.debug) & 4)) flush();
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < 4; ++j) {
             prev[j] = cur[j];
             cur[j] = b[j];
         }
