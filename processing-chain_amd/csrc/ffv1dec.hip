@@ -460,6 +460,7 @@ struct pp_ffv1_dec {
     uint8_t *pkt = nullptr, *states = nullptr, *tables = nullptr;
     int64_t pkt_cap = 0, *soff = nullptr, *slen = nullptr;
     int row_cap = 0;  // widest slice row, rounded to 8 samples
+    int lpw = 16;     // slices per workgroup: 16, fewer when their line buffers would not fit the LDS
     bool q0_alu = false;  // the record's first quantiser is pixpath's (dquant0)
     int *status = nullptr;
     int16_t *dquant = nullptr;
@@ -489,8 +490,9 @@ extern "C" int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extra, int ext
     for (int i = 0; i < D->nh; ++i)
         wmax = std::max(wmax, (int)((int64_t)(i + 1) * w / D->nh - (int64_t)i * w / D->nh));
     D->row_cap = (wmax + 7) / 8 * 8;
-    if ((size_t)D->row_cap * 2 * 64 > kLineLds)
-        PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 decoder: %d-sample slice rows exceed the LDS line buffers", wmax);
+    D->lpw = (int)std::min<size_t>((size_t)ffv1_lanes_per_wave(16), kLineLds / ((size_t)D->row_cap * 2));
+    if (D->lpw < 1)
+        PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 decoder: %d-sample slice rows exceed the LDS line buffer", wmax);
     PP_HIP(hipSetDevice(ctx->device));
     PP_HIP(hipMalloc(&D->states, (size_t)(2 * (int64_t)D->ctx_count * kCtx) * ((ns + 63) / 64 * 64)));  // both halves
     PP_HIP(hipMalloc(&D->soff, sizeof(int64_t) * ns));
@@ -581,7 +583,7 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     a.nh = D->nh; a.nv = D->nv; a.nslices = ns; a.ec = D->ec;
     a.ctx_count = D->ctx_count; a.state_bytes = sb;
     a.states = D->states; a.cold = D->states + half; a.status = D->status; a.tables = D->tables; a.quant = D->dquant;
-    a.lpw = ffv1_lanes_per_wave(16);
+    a.lpw = D->lpw;
     if (const char *e = PP_KNOB("PIXPATH_FFV1_DEBUG")) a.debug = std::atoi(e);
     a.row_cap = D->row_cap;
     static const hipError_t attr = [] {
