@@ -147,32 +147,82 @@ def cgroup_cpus():
         return None
 
 
+ORACLE_SRCS = ("pixoracle.c", "spinner_oracle.c", "siti_oracle.c", "ffv1_oracle.c")
+ORACLE_SCALAR_FLAGS = "gcc -O3 -ffp-contract=off (oracle/Makefile, the parity checker's build)"
+
+
+def oracle_native_build():
+    """The oracle sources built with gcc -O3 -march=native for THIS host (the
+    GPU box's CPU, compiled there: a few seconds), into a temp dir -- the
+    vectorised CPU baseline.  Returns (path, flags) or (None, reason)."""
+    import subprocess
+    import tempfile
+    flags = ["-O3", "-march=native", "-ffp-contract=off", "-fPIC", "-std=c11", "-D_GNU_SOURCE"]
+    out = os.path.join(tempfile.mkdtemp(prefix="pixoracle_native_"), "libpixoracle_native.so")
+    try:
+        subprocess.run(["gcc"] + flags + ["-shared", "-o", out] + [os.path.join(ROOT, "oracle", f) for f in ORACLE_SRCS]
+                       + ["-lm"], check=True, capture_output=True, timeout=180)
+    except (OSError, subprocess.SubprocessError) as e:
+        return None, "native build failed: %s" % e
+    return out, " ".join(["gcc"] + flags)
+
+
+def oracle_modules(lib_path):
+    """Fresh pyoracle / ffv1_ref module instances bound to the oracle build at
+    lib_path (None: oracle/lib/libpixoracle.so)."""
+    import importlib.util
+    old = os.environ.get("PIXORACLE_LIB")
+    if lib_path:
+        os.environ["PIXORACLE_LIB"] = lib_path
+    else:
+        os.environ.pop("PIXORACLE_LIB", None)
+    mods = []
+    try:
+        for name in ("pyoracle", "ffv1_ref"):
+            spec = importlib.util.spec_from_file_location("%s_%s" % (name, "native" if lib_path else "scalar"),
+                                                          os.path.join(ROOT, "oracle", name + ".py"))
+            m = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(m)
+            mods.append(m)
+    finally:
+        if old is None:
+            os.environ.pop("PIXORACLE_LIB", None)
+        else:
+            os.environ["PIXORACLE_LIB"] = old
+    return mods
+
+
 def cpu_baseline(args, wl):
     """Oracle C restatement on host threads (ctypes releases the GIL); the
     scaler and SI/TI are timed separately, the combined rate is per frame that
-    gets both (1 / (1/scale + 1/siti)).  `value` is the rate on EVERY thread of
-    the affinity mask; a shorter sweep over fewer threads is recorded beside."""
+    gets both (1 / (1/scale + 1/siti)).  Two builds of the same sources: gcc
+    -O3 -march=native compiled on this host (vectorised; `value` is its best
+    point of a thread sweep up to every thread of the affinity mask) and the
+    parity checker's scalar -O3 build, timed at the same thread count."""
     import threading
     import numpy as np
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import pyoracle as po
     sfmt, sw, sh, dfmt, dw, dh, flags, siti_wh = wl
     model, nproc, aff = host_cpu()
     full = args.cpu_threads or aff
-    rng = np.random.default_rng(910)
-    sf, df = po.FMT_BY_NAME[sfmt], po.FMT_BY_NAME[dfmt]
-    depth = po.fmt_info(sf)[0]
-    hi = 1024 if depth > 8 else 256
-    # 16 distinct read-only inputs shared by the threads (each has its own Sws scratch)
-    src = [[rng.integers(0, hi, s).astype(po.plane_dtype(sf)) for s in po.plane_shapes(sf, sw, sh)]
-           for _ in range(16)]
-    fl = {"lanczos": po.SWS_LANCZOS, "bicubic": po.SWS_BICUBIC}[flags]
-    sws = [po.Sws(sf, sw, sh, df, dw, dh, fl) for _ in range(full)]
-    outs = [x.out_planes() for x in sws]
-    luma = None
-    if siti_wh:
-        w, h = siti_wh
-        luma = [rng.integers(0, 1024, (4, h, w)).astype(np.uint16) for _ in range(16)]
+    native_path, native_flags = oracle_native_build()
+    po, ffv1_mod = oracle_modules(native_path)
+    po_s, ffv1_s = oracle_modules(None)
+
+    def setup(po, nt):
+        rng = np.random.default_rng(910)
+        sf, df = po.FMT_BY_NAME[sfmt], po.FMT_BY_NAME[dfmt]
+        depth = po.fmt_info(sf)[0]
+        hi = 1024 if depth > 8 else 256
+        # 16 distinct read-only inputs shared by the threads (each has its own Sws scratch)
+        src = [[rng.integers(0, hi, s).astype(po.plane_dtype(sf)) for s in po.plane_shapes(sf, sw, sh)]
+               for _ in range(16)]
+        fl = {"lanczos": po.SWS_LANCZOS, "bicubic": po.SWS_BICUBIC}[flags]
+        sws = [po.Sws(sf, sw, sh, df, dw, dh, fl) for _ in range(nt)]
+        luma = None
+        if siti_wh:
+            w, h = siti_wh
+            luma = [rng.integers(0, 1024, (4, h, w)).astype(np.uint16) for _ in range(16)]
+        return src, sws, [x.out_planes() for x in sws], luma
 
     def timed(fn, nt, secs):
         done = [0] * nt
@@ -188,15 +238,16 @@ def cpu_baseline(args, wl):
             x.join()
         return sum(done), time.perf_counter() - t0
 
-    def do_scale(t):
-        sws[t].scale_into(src[t % 16], outs[t], 4)  # 4 frames per C call
-        return 4
+    def point(po, state, nt, secs):
+        src, sws, outs, luma = state
 
-    def do_siti(t):
-        po.siti_c(luma[t % 16], 10)  # 4 frames: 4 SI + 3 TI
-        return 4
+        def do_scale(t):
+            sws[t].scale_into(src[t % 16], outs[t], 4)  # 4 frames per C call
+            return 4
 
-    def point(nt, secs):
+        def do_siti(t):
+            po.siti_c(luma[t % 16], 10)  # 4 frames: 4 SI + 3 TI
+            return 4
         ns, ts = timed(do_scale, nt, secs)
         r = {"threads": nt, "scale_fps": round(ns / ts, 2), "scale_frames": ns, "scale_s": round(ts, 2)}
         if siti_wh:
@@ -211,36 +262,43 @@ def cpu_baseline(args, wl):
     pts = {int(v) for v in args.cpu_sweep.split(",") if v.strip() and 0 < int(v) < full}
     if quota and int(quota) < full:
         pts.add(int(quota))
-    sweep = [point(k, max(2.0, args.cpu_seconds / 2)) for k in sorted(pts)]
-    widest = point(full, args.cpu_seconds)
+    state = setup(po, full)
+    sweep = [point(po, state, k, max(2.0, args.cpu_seconds / 2)) for k in sorted(pts)]
+    widest = point(po, state, full, args.cpu_seconds)
     sweep.append(widest)
     # value: the best rate this box's host gives the CPU path (the cgroup's CPU
     # quota caps it below the affinity width; more threads than the quota only
     # add contention), with the thread count that reached it
     top = max(sweep, key=lambda r: r["value"])
+    scalar = point(po_s, setup(po_s, top["threads"]), top["threads"], max(2.0, args.cpu_seconds / 2))
+    build = native_flags if native_path else "%s (%s)" % (ORACLE_SCALAR_FLAGS, native_flags)
     out = {"value": top["value"], "unit": "frames/s", "cores": top["threads"], "kind": "port", "host_nproc": nproc,
-           "host_affinity": aff, "cgroup_cpus": quota, "cpu_model": model,
+           "host_affinity": aff, "cgroup_cpus": quota, "cpu_model": model, "build": build,
            "scale_fps": top["scale_fps"], "sweep": sweep,
-           "per_thread_scale_fps": round(top["scale_fps"] / top["threads"], 2)}
+           "per_thread_scale_fps": round(top["scale_fps"] / top["threads"], 2),
+           "scalar": {"build": ORACLE_SCALAR_FLAGS, "value": scalar["value"], "threads": scalar["threads"],
+                      "scale_fps": scalar["scale_fps"], "siti_fps": scalar.get("siti_fps")}}
     if args.workload == "config2":
-        out["e2e"] = cpu_e2e(top["threads"], wl, sws, outs, po, seconds=args.cpu_e2e_seconds)
+        out["e2e"] = cpu_e2e(top["threads"], wl, state[1], state[2], po, ffv1_mod, seconds=args.cpu_e2e_seconds)
+        out["e2e"]["build"] = build
     if siti_wh:
         out["siti_fps"] = top["siti_fps"]
-        out["sample"] = ("%d-thread oracle C restatement (oracle/pixoracle.c + siti_oracle.c, gcc -O3), the best point "
+        out["sample"] = ("%d-thread oracle C restatement (oracle/pixoracle.c + siti_oracle.c, %s), the best point "
                          "of a sweep up to every thread of the affinity mask (%d; the cgroup allows %s CPUs): %d frames "
                          "%dx%d %s -> %dx%d %s %s in %.1f s, then %d frames of %dx%d 10-bit SI/TI in %.1f s; value = "
-                         "per frame that gets both; ffmpeg is absent on the box"
-                         % (top["threads"], full, quota, top["scale_frames"], sw, sh, sfmt, dw, dh, dfmt, flags,
+                         "per frame that gets both; `scalar`: the same at the parity checker's -O3 build; ffmpeg is "
+                         "absent on the box"
+                         % (top["threads"], build, full, quota, top["scale_frames"], sw, sh, sfmt, dw, dh, dfmt, flags,
                             top["scale_s"], top["siti_frames"], siti_wh[0], siti_wh[1], top["siti_s"]))
     else:
-        out["sample"] = ("%d-thread oracle C restatement (gcc -O3), best point of a sweep up to %d threads: %d frames "
+        out["sample"] = ("%d-thread oracle C restatement (%s), best point of a sweep up to %d threads: %d frames "
                          "%dx%d %s -> %dx%d %s %s in %.1f s; ffmpeg is absent on the box"
-                         % (top["threads"], full, top["scale_frames"], sw, sh, sfmt, dw, dh, dfmt, flags,
+                         % (top["threads"], build, full, top["scale_frames"], sw, sh, sfmt, dw, dh, dfmt, flags,
                             top["scale_s"]))
     return out
 
 
-def cpu_e2e(nt, wl, sws, outs, po, seconds=4.0):
+def cpu_e2e(nt, wl, sws, outs, po, ffv1_ref, seconds=4.0):
     """CPU counterpart of e2e_avpvs: per frame, the oracle's scaler then the
     oracle's FFV1 encoder (oracle/ffv1_oracle.c, the same bitstream as the GPU
     encoder, 8x8 slices) on the compressible content e2e_avpvs uses, on nt
@@ -248,8 +306,6 @@ def cpu_e2e(nt, wl, sws, outs, po, seconds=4.0):
     decode and file writes excluded (a lower bound on the CPU time)."""
     import threading
     import numpy as np
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import ffv1_ref
     sfmt, sw, sh, dfmt, dw, dh, flags, _ = wl
     sf = po.FMT_BY_NAME[sfmt]
     rng = np.random.default_rng(77)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PP_ABI_VERSION 5
+#define PP_ABI_VERSION 6
 
 /* return codes */
 #define PP_OK 0
@@ -281,14 +281,21 @@ int pp_ffv1_encode_stats(const pp_ffv1_enc *enc, int *launches);
 int pp_ffv1_encoder_reserve(pp_ffv1_enc *enc, int64_t packet_bytes);
 int pp_ffv1_encoder_memory(const pp_ffv1_enc *enc, int64_t *bytes);
 /* FFV1 decoder (the CPVS stage reads the AVPVS back, lib/ffmpeg.py:1149):
- * version 3 intra streams with the range coder's default state table, one
- * quantisation table set of up to 3 inputs, <= 256 slices, 8/10-bit
- * 4:2:0/4:2:2 -- what pp_ffv1_encode writes.  pp_ffv1_decoder_create parses
- * and checks the configuration record (ctx == NULL: record check only);
- * pp_ffv1_decoder_format gives the PP_FMT_* of the decoded frames;
- * pp_ffv1_decode decodes nframes packets held back to back in HOST memory
- * (frame_sizes[f] bytes each) into dst (device), checking every slice's CRC,
- * header and end position; synchronises `stream`. */
+ * version 3 streams with the range coder (default or transmitted state
+ * table), up to 8 quantisation table sets of up to 5 inputs, initial context
+ * states, intra or inter frames (a GOP's context states carry from frame to
+ * frame), with or without slice CRCs, <= 256 slices, 8/10-bit 4:2:0 / 4:2:2 /
+ * 4:4:4 YCbCr -- what pp_ffv1_encode writes and what `ffmpeg -c:v ffv1 -level 3
+ * -coder 1 -context 1 -slicecrc 1` writes (RFC 9043).  pp_ffv1_decoder_create
+ * parses and checks the configuration record (ctx == NULL: record check
+ * only); pp_ffv1_decoder_format gives the PP_FMT_* of the decoded frames;
+ * pp_ffv1_decode decodes nframes consecutive packets of the stream held back
+ * to back in HOST memory (frame_sizes[f] bytes each) into dst (device),
+ * checking every slice's CRC, header and end position; synchronises
+ * `stream`.  ABI v6: a decode whose first frame is not a keyframe continues
+ * the GOP of the previous successful decode's last frame (its context states
+ * are kept); pp_ffv1_decoder_reset forgets them (after a seek), and such a
+ * decode then fails. */
 typedef struct pp_ffv1_dec pp_ffv1_dec;
 int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extradata, int extradata_size, int w, int h,
                            int max_frames, pp_ffv1_dec **out);
@@ -298,6 +305,13 @@ int pp_ffv1_decoder_format(const pp_ffv1_dec *dec);
 int pp_ffv1_decoder_slices(const pp_ffv1_dec *dec, int *slices_h, int *slices_v);
 int pp_ffv1_decode(pp_ffv1_dec *dec, const uint8_t *packets, const int64_t *frame_sizes, int nframes,
                    const pp_frames *dst, void *stream);
+/* ABI v6.  The record as parsed: up to n of micro_version, coder_type,
+ * quantisation table sets, largest context count, intra, ec, bit mask of the
+ * sets with transmitted initial states, 1 if the tables are pixpath's own
+ * 3-input set; returns the count written. */
+int pp_ffv1_decoder_info(const pp_ffv1_dec *dec, int *info, int n);
+int pp_ffv1_decoder_reset(pp_ffv1_dec *dec);
+int pp_ffv1_decoder_geometry(const pp_ffv1_dec *dec, int *slices_per_workgroup, int *row_cap);
 
 #ifdef __cplusplus
 }

@@ -12,7 +12,9 @@ from fractions import Fraction
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "lib", "libpixoracle.so")
+# PIXORACLE_LIB: another build of the same sources (bench.py's cpu_baseline
+# times a -march=native build beside this scalar one)
+_LIB_PATH = os.environ.get("PIXORACLE_LIB") or os.path.join(_HERE, "lib", "libpixoracle.so")
 
 # format ids (same numbering as include/pixpath.h PP_FMT_*)
 YUV420P, YUV422P, YUV444P, YUV420P10LE, YUV422P10LE, YUV444P10LE, UYVY422, V210 = range(8)

@@ -2,18 +2,23 @@
 // half): reads AVPVS frame packets back into planar frames in HBM for the
 // CPVS stage (create_cpvs decodes the FFV1 AVPVS, lib/ffmpeg.py:1149-1201).
 //
-// Same shape as the encoder (ffv1.hip): ONE LANE PER SLICE over every slice of
-// every frame of the batch.  The host walks each packet's slice footers
-// backwards (24-bit sizes, RFC 9043 4.8) into a slice table; a lane checks
-// its slice's CRC-32 parity, reads the keyframe bit (first slice), the slice
-// header (position from the header, as FFmpeg's decode_slice_header), then
-// decodes Y, Cb, Cr in raster order -- quantised context from the record's
-// tables (LDS), median prediction, get_symbol through the slice's own context
-// states (current context cached in LDS, as in the encoder) -- writing each
-// sample straight into the destination planes, whose previous row it reads
-// back for T / TL / TR.  It finishes with the closing bit at state 129 and
-// FFmpeg's end-of-slice position check.  Per-slice status: 0 ok, 1 CRC,
-// 2 header, 3 end mismatch.
+// Same shape as the encoder (ffv1.hip): ONE LANE PER SLICE CHAIN.  A chain is
+// one slice position over one GOP -- a keyframe and the inter frames after it,
+// whose context states carry over from frame to frame (RFC 9043 4.5; FFmpeg's
+// `-level 3 -coder 1 -context 1` AVPVS of lib/ffmpeg.py:993, :1047 has a GOP
+// of 12); an intra stream (pixpath's own) has one-frame chains, so the batch
+// is frames x slices lanes.  The host walks each packet's slice footers
+// backwards (24-bit sizes, RFC 9043 4.8) into a slice table and reads each
+// frame's keyframe bit to cut the GOPs; a GOP that starts before the batch
+// continues from the states the previous call left (`carry`).  A lane checks
+// its slices' CRC-32 parity, then per frame reads the keyframe bit (first
+// slice), the slice header (position and per-plane quantisation table set,
+// as FFmpeg's decode_slice_header), on a keyframe loads the record's initial
+// states, decodes Y, Cb, Cr in raster order -- quantised context from the
+// record's tables (LDS), median prediction, get_symbol through the slice's
+// context states -- writing each sample straight into the destination planes,
+// and finishes with the closing bit at state 129 and FFmpeg's end-of-slice
+// position check.  Per-slice status: 0 ok, 1 CRC, 2 header, 3 end mismatch.
 #include <algorithm>
 #include <cstring>
 #include <memory>
@@ -27,28 +32,32 @@ namespace pp {
 
 namespace {
 
-constexpr int kCtx = kFfv1CtxBytes;
 constexpr size_t kLineLds = 160 * 1024 - 4096;  // LDS left for line buffers (gfx950: 160 KB per CU)
 
 }  // namespace
 
 struct Ffv1DecArgs {
     const uint8_t *pkt;
-    const int64_t *soff, *slen;  // [nslices] slice start and length (trailer included)
+    const int64_t *soff, *slen;  // [nframes * per] slice start and length (trailer included)
     uint8_t *dst[3];
     int64_t ls[3], fs[3];
-    int w, h, bytes, bits, hsub, vsub, nh, nv, nslices, ec;
-    int ctx_count;               // contexts per plane set (record's tables)
-    int lpw;                     // slices (active lanes) per 64-lane workgroup: ffv1_lanes_per_wave()
-    int row_cap;                 // samples per lane in the LDS line buffer (>= widest slice row)
+    int w, h, bytes, bits, hsub, vsub, nh, nv, per, nchains, ec;
+    const int *gop;              // [nchains / per][3]: first frame, frames, 1 = starts at a keyframe (else carried states)
+    int max_ctx;                 // state slots per plane set (the record's largest table set)
+    int ntables;                 // quantisation table sets in LDS
+    int ctx_count[kFfv1MaxTables];
+    int init_off[kFfv1MaxTables];  // context offset of a set's initial states in `init`, -1: all 128
+    int lpw;                     // chains (active lanes) per 64-lane workgroup
+    int row_cap;                 // samples per lane and row in the LDS line buffers (>= widest slice row)
     int debug;                   // PIXPATH_FFV1_DEBUG (timing ablation only; the output is wrong):
                                  // 2 no CRC check
-    int64_t state_bytes;         // per slice and half: 2 * ctx_count * 16
-    uint8_t *states;             // hot halves [nslices / 64][2 * ctx_count][64][16], primed to 128
+    int64_t state_bytes;         // per chain and half: 2 * max_ctx * 16
+    uint8_t *states;             // hot halves [nchains / 64][2 * max_ctx][64][16]
     uint8_t *cold;               // cold halves, same layout
-    int *status;
-    const uint8_t *tables;       // zero[256], one[256], crc table
-    const int16_t *quant;        // [3][256] (scaled)
+    int *status;                 // [nframes * per], zeroed by the host
+    const uint8_t *tables;       // zero[256], one[256] (the record's), crc table, x^(8 * 2^j)
+    const int16_t *quant;        // [ntables][5][256] (scaled)
+    const uint4 *init;           // [contexts][hot 16 | cold 16] initial states, split as the state halves
 };
 
 // The slice's range decoder (rangecoder.h get_rac / refill) on register-held
@@ -279,174 +288,250 @@ __device__ __forceinline__ int dquant0(int d) {  // d already & 0xFF
     return d < 128 ? q : -q;
 }
 
-template <int BYTES, bool QALU>
+// Copy chain states (both halves, every context) between two slot arrays of
+// the [slot / 64][nctx][64][16] layout: the GOP carried into the next decode.
+__global__ __launch_bounds__(256) void ffv1_state_copy_kernel(const uint8_t *src, int64_t src_half, int src_slot0,
+                                                              uint8_t *dst, int64_t dst_half, int dst_slot0, int nslots,
+                                                              int nctx) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_half = (int64_t)nslots * nctx;
+    if (i >= 2 * per_half) return;
+    const int half = (int)(i / per_half);
+    const int64_t r = i - half * per_half;
+    const int slot = (int)(r % nslots), k = (int)(r / nslots);
+    auto at = [&](int sl) { return (int64_t)(sl >> 6) * (64 * (int64_t)nctx * 16) + (int64_t)k * 1024 + (sl & 63) * 16; };
+    const uint4 v = *reinterpret_cast<const uint4 *>(src + half * src_half + at(src_slot0 + slot));
+    *reinterpret_cast<uint4 *>(dst + half * dst_half + at(dst_slot0 + slot)) = v;
+}
+
+// PIX: the record is pixpath's own 3-input set (first quantiser as ALU code,
+// one LDS line row per lane); else the general 5-input context
+// (ffv1_template.c get_context) over two line rows -- the row above and the
+// row two above, which the current row overwrites in place (decode_plane's
+// sample buffers).  A set whose inputs 4 and 5 are unused has all-zero tables
+// there (read_quant_table: non-decreasing levels from 0), so the sum is the
+// 3-input context.
+template <int BYTES, bool PIX>
 __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
     __shared__ uint8_t s_tab[512];  // zero[256], one[256]
     __shared__ uint32_t s_crc[256];
-    __shared__ int16_t s_q[3][256];
     __shared__ uint32_t s_xp[32];   // x^(8 * 2^j) mod P
-    extern __shared__ __align__(16) uint16_t s_line[];  // [lpw][row_cap]: the row above, per slice
+    extern __shared__ __align__(16) int16_t s_dyn[];  // [ntables][5][256] quantisers, then [lpw][rows][row_cap] lines
     const int lane = threadIdx.x;
     for (int i = lane; i < 256; i += blockDim.x) {
         s_tab[i] = a.tables[i];
         s_tab[256 + i] = a.tables[256 + i];
         s_crc[i] = reinterpret_cast<const uint32_t *>(a.tables + 512)[i];
-        s_q[0][i] = a.quant[i];
-        s_q[1][i] = a.quant[256 + i];
-        s_q[2][i] = a.quant[512 + i];
     }
+    const int nq = a.ntables * 5 * 256;
+    for (int i = lane; i < nq; i += blockDim.x) s_dyn[i] = a.quant[i];
     if (lane < 32) s_xp[lane] = reinterpret_cast<const uint32_t *>(a.tables + 1536)[lane];
     __syncthreads();
-    const int g = blockIdx.x * a.lpw + lane;
+    const int c = blockIdx.x * a.lpw + lane;  // this lane's chain
     if (a.ec && !(PP_ABLATE(a.debug) & 2)) {
         // CRC-32 parity of each slice, trailer included, must leave 0.  The
         // whole wave checks one slice at a time: lane t takes the t-th 64th
         // of its bytes, and its remainder moves past the bytes after them
         // (times x^(8 m) mod P) before the XOR over the wave -- the CRC is
         // linear in the message.
-        bool crc_bad = false;
-        for (int j = 0; j < a.lpw; ++j) {
-            const int gj = blockIdx.x * a.lpw + j;
-            if (gj >= a.nslices) break;
-            const uint8_t *const sj = a.pkt + a.soff[gj];
-            const int nj = (int)a.slen[gj];
-            const int C = (nj + 63) / 64;
-            const int b0 = min(nj, lane * C), b1 = min(nj, b0 + C);
-            uint32_t crc = 0;
+        int bad_j = -1;
+        for (int t = 0; t < a.lpw; ++t) {
+            const int ct = blockIdx.x * a.lpw + t;
+            if (ct >= a.nchains) break;
+            const int kt = ct / a.per, st_ = ct - kt * a.per;
+            const int f0t = a.gop[3 * kt], nft = a.gop[3 * kt + 1];
+            for (int j = 0; j < nft; ++j) {
+                const int64_t gj = (int64_t)(f0t + j) * a.per + st_;
+                const uint8_t *const sj = a.pkt + a.soff[gj];
+                const int nj = (int)a.slen[gj];
+                const int C = (nj + 63) / 64;
+                const int b0 = min(nj, lane * C), b1 = min(nj, b0 + C);
+                uint32_t crc = 0;
 #pragma unroll 8
-            for (int i = b0; i < b1; ++i) crc = (crc << 8) ^ s_crc[(crc >> 24) ^ sj[i]];
-            for (int k = 0, m = nj - b1; m; ++k, m >>= 1)
-                if (m & 1) crc = gf2_mulmod(crc, s_xp[k]);
+                for (int i = b0; i < b1; ++i) crc = (crc << 8) ^ s_crc[(crc >> 24) ^ sj[i]];
+                for (int k = 0, m = nj - b1; m; ++k, m >>= 1)
+                    if (m & 1) crc = gf2_mulmod(crc, s_xp[k]);
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, o, 64);
-            if (lane == j) crc_bad = crc != 0;
+                for (int o = 32; o >= 1; o >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, o, 64);
+                if (lane == t && crc != 0 && bad_j < 0) bad_j = j;
+            }
         }
-        if (lane < a.lpw && g < a.nslices && crc_bad) {
-            a.status[g] = 1;
+        if (lane < a.lpw && c < a.nchains && bad_j >= 0) {
+            const int kc = c / a.per;
+            a.status[(int64_t)(a.gop[3 * kc] + bad_j) * a.per + (c - kc * a.per)] = 1;
             return;
         }
     }
-    if (lane >= a.lpw || g >= a.nslices) return;
-    const int per = a.nh * a.nv;
-    const int frame = g / per, s = g - frame * per;
-    const uint8_t *const sb = a.pkt + a.soff[g];
-    const int64_t n = a.slen[g];
-    uint16_t *const line = s_line + lane * a.row_cap;
-    // context states of 64 neighbouring slices interleaved by slice (as the
-    // encoder's): context k of slice g at [g / 64][k][g % 64], so a context
+    if (lane >= a.lpw || c >= a.nchains) return;
+    const int kg = c / a.per, s = c - kg * a.per;
+    const int f0 = a.gop[3 * kg], nf = a.gop[3 * kg + 1], key_start = a.gop[3 * kg + 2] & 1;
+    uint16_t *const lines = reinterpret_cast<uint16_t *>(s_dyn + nq) + lane * a.row_cap * (PIX ? 1 : 2);
+    // context states of 64 neighbouring chains interleaved by chain (as the
+    // encoder's): context k of chain c at [c / 64][k][c % 64], so a context
     // that is hot in neighbouring slices -- the same picture content -- shares
     // their 128-B lines in L2 instead of one line per slice
-    uint8_t *const st0 = a.states + (int64_t)(g >> 6) * (64 * a.state_bytes) + (g & 63) * 16;
-    uint8_t *const co0 = a.cold + (int64_t)(g >> 6) * (64 * a.state_bytes) + (g & 63) * 16;
+    uint8_t *const st0 = a.states + (int64_t)(c >> 6) * (64 * a.state_bytes) + (c & 63) * 16;
+    uint8_t *const co0 = a.cold + (int64_t)(c >> 6) * (64 * a.state_bytes) + (c & 63) * 16;
     constexpr int kCtxStride = 64 * 16;
-    Dec d;
-    {
-        // pkt is 256-B aligned: the slice's misalignment is its offset's
-        const int off = (int)(a.soff[g] & 3);
-        d.w = reinterpret_cast<const uint32_t *>(sb - off);
-        d.end = off + (int)n;
-        d.range = 0xFF00;
-        d.low = n >= 2 ? ((uint32_t)sb[0] << 8) | sb[1] : 0;
-        d.pos = off + 2;
-        if (d.low >= 0xFF00u) { d.low = 0xFF00u; d.end = d.pos; }
-        d.cur = d.w[d.pos >> 2];
-        dec_prefetch(d);
-    }
-    uint32_t dummy;
-    if (s == 0 && !dec_rac(d, 128, s_tab, dummy)) {  // keyframe bit
-        a.status[g] = 2;
-        return;
-    }
-    bool bad = false;
-    int hv[9];
-    {
-        uint32_t hb[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) hb[i] = 0x80808080u;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) hv[i] = dec_symbol<false>(d, hb, s_tab, bad);
-    }
-    const int sx = hv[0], sy = hv[1], sw = hv[2] + 1, sh = hv[3] + 1;
-    if (bad || sx < 0 || sy < 0 || sx > a.nh - sw || sy > a.nv - sh || hv[4] || hv[5] || hv[6] != 3) {
-        a.status[g] = 2;
-        return;
-    }
-    const int x0 = (int)((int64_t)sx * a.w / a.nh), x1 = (int)((int64_t)(sx + sw) * a.w / a.nh);
-    const int y0 = (int)((int64_t)sy * a.h / a.nv), y1 = (int)((int64_t)(sy + sh) * a.h / a.nv);
-    if (x1 - x0 > a.row_cap) {  // wider than this grid's slices
-        a.status[g] = 2;
-        return;
-    }
     const int mask = (1 << a.bits) - 1;
-    int cur_key = 0;  // context 0 holding its initial states: the first write-back rewrites 128s
-    uint32_t blk[4] = {0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u};
-    for (int p = 0; p < 3; p++) {
-        const int pw = p ? ((x1 - x0) + (1 << a.hsub) - 1) >> a.hsub : x1 - x0;
-        const int ph = p ? ((y1 - y0) + (1 << a.vsub) - 1) >> a.vsub : y1 - y0;
-        const int px0 = p ? x0 >> a.hsub : x0, py0 = p ? y0 >> a.vsub : y0;
-        uint8_t *dp = p == 0 ? a.dst[0] : p == 1 ? a.dst[1] : a.dst[2];
-        const int64_t ls = p == 0 ? a.ls[0] : p == 1 ? a.ls[1] : a.ls[2];
-        const int64_t fs = p == 0 ? a.fs[0] : p == 1 ? a.fs[1] : a.fs[2];
-        uint8_t *base = dp + frame * fs + (int64_t)py0 * ls + (int64_t)px0 * BYTES;
-        const int key0 = p ? a.ctx_count : 0;
-        int T0prev = 0;  // the row above's first sample, one row later: TL at a row start
-        auto put = [&](uint8_t *r, int xx, int vv) {
-            if (BYTES == 2)
-                reinterpret_cast<uint16_t *>(r)[xx] = (uint16_t)vv;
-            else
-                r[xx] = (uint8_t)vv;
-        };
-        int pv = 0;
-        for (int y = 0; y < ph; y++) {
-            uint8_t *row = base + (int64_t)y * ls;
-            // `line` holds the row above (never read for the first row); sample
-            // x overwrites line[x] once it is no longer needed as T / TR
-            int T = y > 0 ? line[0] : 0;
-            int TL = y > 1 ? T0prev : 0;
-            T0prev = T;
-            int L = T;
-            // the row above two columns ahead, read a sample early
-            int TR = pw > 1 ? (y > 0 ? line[1] : 0) : T;
-            for (int x = 0; x < pw; x++) {
-                const int nTR = x + 2 < pw ? (y > 0 ? line[x + 2] : 0) : TR;
-                int ctx = (QALU ? dquant0((L - TL) & 0xFF) : s_q[0][(L - TL) & 0xFF]) + s_q[1][(TL - T) & 0xFF] +
-                          s_q[2][(T - TR) & 0xFF];
-                const bool neg = ctx < 0;
-                if (neg) ctx = -ctx;
-                const int key = key0 + ctx;
-                dec_prefetch(d);
-                // Branch-free: memory operations complete in issue order, so the
-                // block load goes out before the previous sample's store and the
-                // write-back of the current block, and waiting for it does not
-                // wait for their acks.  Same context: the load is stale and the
-                // registers are kept.
-                {
-                    const uint4 nb = *reinterpret_cast<const uint4 *>(st0 + key * kCtxStride);
-                    // (x = 0: the previous row's last sample lands on row[0] until x = 1 rewrites it)
-                    put(row, max(x - 1, 0), pv);
-                    *reinterpret_cast<uint4 *>(st0 + cur_key * kCtxStride) = make_uint4(blk[0], blk[1], blk[2], blk[3]);
-                    const bool same = key == cur_key;
-                    blk[0] = same ? blk[0] : nb.x;
-                    blk[1] = same ? blk[1] : nb.y;
-                    blk[2] = same ? blk[2] : nb.z;
-                    blk[3] = same ? blk[3] : nb.w;
-                    cur_key = key;
+    for (int j = 0; j < nf; ++j) {
+        const int64_t g = (int64_t)(f0 + j) * a.per + s;  // (frame, slice) of this step
+        const uint8_t *const sb = a.pkt + a.soff[g];
+        const int64_t n = a.slen[g];
+        Dec d;
+        {
+            // pkt is 256-B aligned: the slice's misalignment is its offset's
+            const int off = (int)(a.soff[g] & 3);
+            d.w = reinterpret_cast<const uint32_t *>(sb - off);
+            d.end = off + (int)n;
+            d.range = 0xFF00;
+            d.low = n >= 2 ? ((uint32_t)sb[0] << 8) | sb[1] : 0;
+            d.pos = off + 2;
+            if (d.low >= 0xFF00u) { d.low = 0xFF00u; d.end = d.pos; }
+            d.cur = d.w[d.pos >> 2];
+            dec_prefetch(d);
+        }
+        uint32_t dummy;
+        const bool key = j == 0 && key_start;
+        if (s == 0 && dec_rac(d, 128, s_tab, dummy) != (key ? 1u : 0u)) {  // keyframe bit
+            a.status[g] = 2;
+            return;
+        }
+        bool bad = false;
+        int hv[9];
+        {
+            uint32_t hb[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) hb[i] = 0x80808080u;
+#pragma unroll
+            for (int i = 0; i < 9; ++i) hv[i] = dec_symbol<false>(d, hb, s_tab, bad);
+        }
+        const int sx = hv[0], sy = hv[1], sw = hv[2] + 1, sh = hv[3] + 1;
+        if (bad || sx < 0 || sy < 0 || sx > a.nh - sw || sy > a.nv - sh || hv[4] < 0 || hv[4] >= a.ntables ||
+            hv[5] < 0 || hv[5] >= a.ntables || (PIX && (hv[4] || hv[5]))) {
+            a.status[g] = 2;
+            return;
+        }
+        const int x0 = (int)((int64_t)sx * a.w / a.nh), x1 = (int)((int64_t)(sx + sw) * a.w / a.nh);
+        const int y0 = (int)((int64_t)sy * a.h / a.nv), y1 = (int)((int64_t)(sy + sh) * a.h / a.nv);
+        if (x1 - x0 > a.row_cap) {  // wider than this grid's slices
+            a.status[g] = 2;
+            return;
+        }
+        if (key) {  // ff_ffv1_clear_slice_state: the set's initial states (the host primed 128s)
+            for (int p = 0; p < 2; ++p) {
+                const int ti = hv[4 + p], io = a.init_off[ti];
+                if (io < 0) continue;
+                for (int q = 0; q < a.ctx_count[ti]; ++q) {
+                    const uint4 hot = a.init[2 * (int64_t)(io + q)], cold = a.init[2 * (int64_t)(io + q) + 1];
+                    *reinterpret_cast<uint4 *>(st0 + (p * a.max_ctx + q) * kCtxStride) = hot;
+                    *reinterpret_cast<uint4 *>(co0 + (p * a.max_ctx + q) * kCtxStride) = cold;
                 }
-                int diff = dec_symbol_split<true>(d, blk, co0 + cur_key * kCtxStride, s_tab, bad);
-                if (neg) diff = -diff;
-                const int v = (dmedian3(L, L + T - TL, T) + diff) & mask;
-                pv = v;  // stored during the next sample, after its block load
-                line[x] = (uint16_t)v;
-                TL = T;
-                T = TR;
-                TR = nTR;
-                L = v;
             }
-            if (pw > 0) put(row, pw - 1, pv);
+        }
+        // the block of context 0 in registers (every switch writes the held
+        // block back, so it must start as the stored one)
+        int cur_key = 0;
+        uint32_t blk[4];
+        {
+            const uint4 b0 = *reinterpret_cast<const uint4 *>(st0);
+            blk[0] = b0.x; blk[1] = b0.y; blk[2] = b0.z; blk[3] = b0.w;
+        }
+        for (int p = 0; p < 3; p++) {
+            const int pw = p ? ((x1 - x0) + (1 << a.hsub) - 1) >> a.hsub : x1 - x0;
+            const int ph = p ? ((y1 - y0) + (1 << a.vsub) - 1) >> a.vsub : y1 - y0;
+            const int px0 = p ? x0 >> a.hsub : x0, py0 = p ? y0 >> a.vsub : y0;
+            uint8_t *dp = p == 0 ? a.dst[0] : p == 1 ? a.dst[1] : a.dst[2];
+            const int64_t ls = p == 0 ? a.ls[0] : p == 1 ? a.ls[1] : a.ls[2];
+            const int64_t fs = p == 0 ? a.fs[0] : p == 1 ? a.fs[1] : a.fs[2];
+            uint8_t *base = dp + (int64_t)(f0 + j) * fs + (int64_t)py0 * ls + (int64_t)px0 * BYTES;
+            const int key0 = p ? a.max_ctx : 0;
+            const int16_t *const q = s_dyn + hv[4 + (p ? 1 : 0)] * (5 * 256);
+            auto put = [&](uint8_t *r, int xx, int vv) {
+                if (BYTES == 2)
+                    reinterpret_cast<uint16_t *>(r)[xx] = (uint16_t)vv;
+                else
+                    r[xx] = (uint8_t)vv;
+            };
+            int pv = 0;
+            int T0prev = 0;  // PIX: the row above's first sample, one row later: TL at a row start
+            // general: `up` holds the row above, `two` the row two above, which
+            // the current row overwrites sample by sample (TT read first)
+            uint16_t *up = lines, *two = PIX ? lines : lines + a.row_cap;
+            for (int y = 0; y < ph; y++) {
+                uint8_t *row = base + (int64_t)y * ls;
+                // the row above is never read for the first row (nor the row two above for the first two)
+                int T = y > 0 ? up[0] : 0;
+                int TL;
+                if constexpr (PIX) {
+                    TL = y > 1 ? T0prev : 0;
+                    T0prev = T;
+                } else {
+                    TL = y > 1 ? two[0] : 0;
+                }
+                int L = T, LL = 0;
+                // the row above two columns ahead, read a sample early
+                int TR = pw > 1 ? (y > 0 ? up[1] : 0) : T;
+                int TT = (!PIX && y > 1) ? two[0] : 0;
+                for (int x = 0; x < pw; x++) {
+                    const int nTR = x + 2 < pw ? (y > 0 ? up[x + 2] : 0) : TR;
+                    int nTT = 0;
+                    if constexpr (!PIX) nTT = (y > 1 && x + 1 < pw) ? two[x + 1] : 0;
+                    int ctx;
+                    if constexpr (PIX)
+                        ctx = dquant0((L - TL) & 0xFF) + q[256 + ((TL - T) & 0xFF)] + q[512 + ((T - TR) & 0xFF)];
+                    else
+                        ctx = q[(L - TL) & 0xFF] + q[256 + ((TL - T) & 0xFF)] + q[512 + ((T - TR) & 0xFF)] +
+                              q[768 + ((LL - L) & 0xFF)] + q[1024 + ((TT - T) & 0xFF)];
+                    const bool neg = ctx < 0;
+                    if (neg) ctx = -ctx;
+                    const int key = key0 + ctx;
+                    dec_prefetch(d);
+                    // Branch-free: memory operations complete in issue order, so the
+                    // block load goes out before the previous sample's store and the
+                    // write-back of the current block, and waiting for it does not
+                    // wait for their acks.  Same context: the load is stale and the
+                    // registers are kept.
+                    {
+                        const uint4 nb = *reinterpret_cast<const uint4 *>(st0 + key * kCtxStride);
+                        // (x = 0: the previous row's last sample lands on row[0] until x = 1 rewrites it)
+                        put(row, max(x - 1, 0), pv);
+                        *reinterpret_cast<uint4 *>(st0 + cur_key * kCtxStride) = make_uint4(blk[0], blk[1], blk[2], blk[3]);
+                        const bool same = key == cur_key;
+                        blk[0] = same ? blk[0] : nb.x;
+                        blk[1] = same ? blk[1] : nb.y;
+                        blk[2] = same ? blk[2] : nb.z;
+                        blk[3] = same ? blk[3] : nb.w;
+                        cur_key = key;
+                    }
+                    int diff = dec_symbol_split<true>(d, blk, co0 + cur_key * kCtxStride, s_tab, bad);
+                    if (neg) diff = -diff;
+                    const int v = (dmedian3(L, L + T - TL, T) + diff) & mask;
+                    pv = v;  // stored during the next sample, after its block load
+                    two[x] = (uint16_t)v;  // PIX: `two` is the one line (x is no longer T or TR)
+                    TL = T;
+                    T = TR;
+                    TR = nTR;
+                    LL = L;
+                    L = v;
+                    TT = nTT;
+                }
+                if (pw > 0) put(row, pw - 1, pv);
+                if constexpr (!PIX) {
+                    uint16_t *t = up;
+                    up = two;
+                    two = t;
+                }
+            }
+        }
+        *reinterpret_cast<uint4 *>(st0 + cur_key * kCtxStride) = make_uint4(blk[0], blk[1], blk[2], blk[3]);
+        (void)dec_rac(d, 129, s_tab, dummy);  // the closing bit at state 129
+        const int st = bad ? 2 : ((d.end - d.pos) - 2 - 5 * (a.ec != 0)) != 0 ? 3 : 0;
+        if (st) {
+            a.status[g] = st;
+            return;
         }
     }
-    (void)dec_rac(d, 129, s_tab, dummy);  // the closing bit at state 129
-    a.status[g] = bad ? 2 : ((d.end - d.pos) - 2 - 5 * (a.ec != 0)) != 0 ? 3 : 0;
 }
 
 }  // namespace pp
@@ -455,53 +540,103 @@ using namespace pp;
 
 struct pp_ffv1_dec {
     pp_ctx *ctx = nullptr;
-    int w = 0, h = 0, bits = 8, hsub = 1, vsub = 1, nh = 1, nv = 1, ec = 0, max_frames = 0, ctx_count = 0;
-    int16_t quant[3][256];
-    uint8_t *pkt = nullptr, *states = nullptr, *tables = nullptr;
+    int w = 0, h = 0, max_frames = 0;
+    Ffv1Record rec;
+    bool pix = false;  // pixpath's own 3-input set (ALU first quantiser, one line row)
+    uint8_t *pkt = nullptr, *states = nullptr, *tables = nullptr, *carry = nullptr;
     int64_t pkt_cap = 0, *soff = nullptr, *slen = nullptr;
+    int *gop = nullptr;
     int row_cap = 0;  // widest slice row, rounded to 8 samples
-    int lpw = 16;     // slices per workgroup: 16, fewer when their line buffers would not fit the LDS
-    bool q0_alu = false;  // the record's first quantiser is pixpath's (dquant0)
+    int lpw = 16;     // chains per workgroup: 16, fewer when their line buffers would not fit the LDS
+    size_t lds = 0;   // dynamic LDS per workgroup at lpw: quantisers + line rows
     int *status = nullptr;
     int16_t *dquant = nullptr;
+    uint4 *dinit = nullptr;
+    int init_off[kFfv1MaxTables];
+    int64_t slots = 0;        // chain state slots allocated (64-aligned)
+    bool carry_valid = false; // `carry` holds the last GOP's states of the previous decode
 };
+
+namespace {
+
+// a context's 32 FFmpeg state bytes -> the HOT | COLD halves of the decoder
+// (dec_symbol_split): HOT [0] zero, [1..5] exponent 0..4, [6..10] sign e = 0..4,
+// [11..14] mantissa 0..3; COLD [0..4] exponent 5..9, [5..9] sign e = 5..9,
+// [10..14] mantissa 4..8 (states 21 and 31 serve > 10-bit samples only)
+void split_states(const uint8_t *st, uint8_t hot[16], uint8_t cold[16]) {
+    std::memset(hot, 128, 16);
+    std::memset(cold, 128, 16);
+    hot[0] = st[0];
+    for (int i = 0; i < 5; ++i) {
+        hot[1 + i] = st[1 + i];
+        hot[6 + i] = st[11 + i];
+        cold[i] = st[6 + i];
+        cold[5 + i] = st[16 + i];
+        cold[10 + i] = st[26 + i];
+    }
+    for (int i = 0; i < 4; ++i) hot[11 + i] = st[22 + i];
+}
+
+bool pixpath_tables(const Ffv1Record &r) {
+    if (r.ntables != 1) return false;
+    for (int i = 0; i < 256; ++i)
+        if (r.quant[0][0][i] != ffv1_quant(i) || r.quant[0][1][i] != 11 * ffv1_quant(i) ||
+            r.quant[0][2][i] != 121 * ffv1_quant(i) || r.quant[0][3][i] || r.quant[0][4][i])
+            return false;
+    return true;
+}
+
+}  // namespace
 
 extern "C" int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extra, int extra_size, int w, int h,
                                       int max_frames, pp_ffv1_dec **out) {
     if (!out || !extra) PP_FAIL(PP_ERR_INVALID, "null argument");
     *out = nullptr;
     if (w < 2 || h < 2 || max_frames < 1) PP_FAIL(PP_ERR_INVALID, "bad size %dx%d / max_frames %d", w, h, max_frames);
-    Ffv1Record rec;
-    std::string err;
-    if (int rc = ffv1_parse_record(extra, extra_size, w, h, &rec, &err)) PP_FAIL(rc, "%s", err.c_str());
     std::unique_ptr<pp_ffv1_dec> D(new pp_ffv1_dec());
+    std::string err;
+    if (int rc = ffv1_parse_record(extra, extra_size, w, h, &D->rec, &err)) PP_FAIL(rc, "%s", err.c_str());
+    const Ffv1Record &R = D->rec;
+    if (R.bits != 8 && R.bits != 10) PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 decoder: %d-bit samples (8 or 10)", R.bits);
+    if (R.hsub == 0 && R.vsub == 1) PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 decoder: 4:4:0 chroma");
     D->ctx = ctx; D->w = w; D->h = h; D->max_frames = max_frames;
-    D->bits = rec.bits; D->hsub = rec.hsub; D->vsub = rec.vsub; D->nh = rec.nh; D->nv = rec.nv; D->ec = rec.ec;
-    D->ctx_count = rec.ctx_count;
-    std::memcpy(D->quant, rec.quant, sizeof(D->quant));
-    D->q0_alu = true;
-    for (int i = 0; i < 256; ++i) D->q0_alu = D->q0_alu && D->quant[0][i] == ffv1_quant(i);
+    D->pix = pixpath_tables(R);
+    int wmax = 0;
+    for (int i = 0; i < R.nh; ++i)
+        wmax = std::max(wmax, (int)((int64_t)(i + 1) * w / R.nh - (int64_t)i * w / R.nh));
+    D->row_cap = (wmax + 7) / 8 * 8;
+    const size_t qbytes = (size_t)R.ntables * 5 * 256 * 2, rows = D->pix ? 1 : 2;
+    const size_t per_lane = (size_t)D->row_cap * 2 * rows;
+    D->lpw = qbytes + per_lane > kLineLds
+                 ? 0
+                 : (int)std::min<size_t>((size_t)ffv1_lanes_per_wave(16), (kLineLds - qbytes) / per_lane);
+    if (D->lpw < 1)
+        PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 decoder: %d-sample slice rows exceed the LDS line buffer", wmax);
+    int ninit = 0;
+    for (int t = 0; t < R.ntables; ++t) {
+        D->init_off[t] = R.init[t].empty() ? -1 : ninit;
+        ninit += R.init[t].empty() ? 0 : R.ctx_count[t];
+    }
     if (!ctx) {
         *out = D.release();
         return PP_OK;
     }
-    const int64_t ns = (int64_t)D->nh * D->nv * max_frames;
-    int wmax = 0;
-    for (int i = 0; i < D->nh; ++i)
-        wmax = std::max(wmax, (int)((int64_t)(i + 1) * w / D->nh - (int64_t)i * w / D->nh));
-    D->row_cap = (wmax + 7) / 8 * 8;
-    D->lpw = (int)std::min<size_t>((size_t)ffv1_lanes_per_wave(16), kLineLds / ((size_t)D->row_cap * 2));
-    if (D->lpw < 1)
-        PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 decoder: %d-sample slice rows exceed the LDS line buffer", wmax);
+    const int per = R.nh * R.nv;
+    D->slots = ((int64_t)per * max_frames + 63) / 64 * 64;
+    const int64_t half = 2 * (int64_t)R.max_ctx * 16 * D->slots;
+    const int64_t chalf = 2 * (int64_t)R.max_ctx * 16 * ((per + 63) / 64 * 64);
     PP_HIP(hipSetDevice(ctx->device));
-    PP_HIP(hipMalloc(&D->states, (size_t)(2 * (int64_t)D->ctx_count * kCtx) * ((ns + 63) / 64 * 64)));  // both halves
-    PP_HIP(hipMalloc(&D->soff, sizeof(int64_t) * ns));
-    PP_HIP(hipMalloc(&D->slen, sizeof(int64_t) * ns));
-    PP_HIP(hipMalloc(&D->status, sizeof(int) * ns));
+    PP_HIP(hipMalloc(&D->states, 2 * half));  // both halves
+    PP_HIP(hipMalloc(&D->carry, 2 * chalf));
+    PP_HIP(hipMalloc(&D->soff, sizeof(int64_t) * per * max_frames));
+    PP_HIP(hipMalloc(&D->slen, sizeof(int64_t) * per * max_frames));
+    PP_HIP(hipMalloc(&D->status, sizeof(int) * per * max_frames));
+    PP_HIP(hipMalloc(&D->gop, sizeof(int) * 3 * max_frames));
     PP_HIP(hipMalloc(&D->tables, 512 + 1024 + 128));
-    PP_HIP(hipMalloc(&D->dquant, sizeof(D->quant)));
+    PP_HIP(hipMalloc(&D->dquant, qbytes));
     uint8_t tab[512 + 1024 + 128];
-    rac_states(tab, tab + 256);
+    std::memcpy(tab, R.zero_state, 256);
+    std::memcpy(tab + 256, R.one_state, 256);
     crc_table(reinterpret_cast<uint32_t *>(tab + 512));
     {  // x^(8 * 2^j) mod P by squaring, from x^8
         uint32_t *xp = reinterpret_cast<uint32_t *>(tab + 1536);
@@ -517,32 +652,68 @@ extern "C" int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extra, int ext
         for (int j = 1; j < 32; ++j) xp[j] = mulmod(xp[j - 1], xp[j - 1]);
     }
     PP_HIP(hipMemcpy(D->tables, tab, sizeof(tab), hipMemcpyHostToDevice));
-    PP_HIP(hipMemcpy(D->dquant, D->quant, sizeof(D->quant), hipMemcpyHostToDevice));
+    PP_HIP(hipMemcpy(D->dquant, R.quant, qbytes, hipMemcpyHostToDevice));
+    if (ninit) {
+        std::vector<uint8_t> split((size_t)ninit * 32);
+        for (int t = 0; t < R.ntables; ++t)
+            for (int k = 0; D->init_off[t] >= 0 && k < R.ctx_count[t]; ++k) {
+                uint8_t *o = split.data() + (size_t)(D->init_off[t] + k) * 32;
+                split_states(R.init[t].data() + (size_t)k * 32, o, o + 16);
+            }
+        PP_HIP(hipMalloc(&D->dinit, split.size()));
+        PP_HIP(hipMemcpy(D->dinit, split.data(), split.size(), hipMemcpyHostToDevice));
+    }
     *out = D.release();
     return PP_OK;
 }
 
 extern "C" int pp_ffv1_decoder_destroy(pp_ffv1_dec *D) {
     if (!D) return PP_OK;
-    for (void *p : {(void *)D->pkt, (void *)D->states, (void *)D->soff, (void *)D->slen, (void *)D->status,
-                    (void *)D->tables, (void *)D->dquant})
+    for (void *p : {(void *)D->pkt, (void *)D->states, (void *)D->carry, (void *)D->soff, (void *)D->slen,
+                    (void *)D->status, (void *)D->gop, (void *)D->tables, (void *)D->dquant, (void *)D->dinit})
         if (p) (void)hipFree(p);
     delete D;
     return PP_OK;
 }
 
-// Format of the decoded frames (PP_FMT_*), from the configuration record.
-extern "C" int pp_ffv1_decoder_slices(const pp_ffv1_dec *D, int *slices_h, int *slices_v) {
-    if (!D || !slices_h || !slices_v) PP_FAIL(PP_ERR_INVALID, "null argument");
-    *slices_h = D->nh;
-    *slices_v = D->nv;
+extern "C" int pp_ffv1_decoder_geometry(const pp_ffv1_dec *D, int *slices_per_workgroup, int *row_cap) {
+    if (!D || !slices_per_workgroup || !row_cap) PP_FAIL(PP_ERR_INVALID, "null argument");
+    *slices_per_workgroup = D->lpw;
+    *row_cap = D->row_cap;
     return PP_OK;
 }
 
+extern "C" int pp_ffv1_decoder_slices(const pp_ffv1_dec *D, int *slices_h, int *slices_v) {
+    if (!D || !slices_h || !slices_v) PP_FAIL(PP_ERR_INVALID, "null argument");
+    *slices_h = D->rec.nh;
+    *slices_v = D->rec.nv;
+    return PP_OK;
+}
+
+// Format of the decoded frames (PP_FMT_*), from the configuration record.
 extern "C" int pp_ffv1_decoder_format(const pp_ffv1_dec *D) {
     if (!D) PP_FAIL(PP_ERR_INVALID, "null decoder");
-    if (D->bits == 8) return D->vsub ? PP_FMT_YUV420P : PP_FMT_YUV422P;
-    return D->vsub ? PP_FMT_YUV420P10LE : PP_FMT_YUV422P10LE;
+    const Ffv1Record &R = D->rec;
+    if (R.hsub == 0) return R.bits == 8 ? PP_FMT_YUV444P : PP_FMT_YUV444P10LE;
+    if (R.bits == 8) return R.vsub ? PP_FMT_YUV420P : PP_FMT_YUV422P;
+    return R.vsub ? PP_FMT_YUV420P10LE : PP_FMT_YUV422P10LE;
+}
+
+extern "C" int pp_ffv1_decoder_info(const pp_ffv1_dec *D, int *info, int n) {
+    if (!D || !info || n < 0) PP_FAIL(PP_ERR_INVALID, "null argument");
+    const Ffv1Record &R = D->rec;
+    int has_init = 0;
+    for (int t = 0; t < R.ntables; ++t) has_init |= (!R.init[t].empty()) << t;
+    const int v[] = {R.micro, R.coder, R.ntables, R.max_ctx, R.intra, R.ec, has_init, D->pix ? 1 : 0};
+    const int k = std::min<int>(n, (int)(sizeof(v) / sizeof(v[0])));
+    for (int i = 0; i < k; ++i) info[i] = v[i];
+    return k;
+}
+
+extern "C" int pp_ffv1_decoder_reset(pp_ffv1_dec *D) {
+    if (!D) PP_FAIL(PP_ERR_INVALID, "null decoder");
+    D->carry_valid = false;
+    return PP_OK;
 }
 
 extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int64_t *frame_sizes, int nframes,
@@ -551,14 +722,29 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     if (!D->ctx) PP_FAIL(PP_ERR_INVALID, "host-only decoder cannot decode");
     if (nframes > D->max_frames) PP_FAIL(PP_ERR_INVALID, "%d frames > max_frames %d", nframes, D->max_frames);
     if (nframes == 0) return PP_OK;
+    const Ffv1Record &R = D->rec;
     hipStream_t st = static_cast<hipStream_t>(stream);
     PP_HIP(hipSetDevice(D->ctx->device));
-    const int per = D->nh * D->nv, ns = per * nframes;
+    const int per = R.nh * R.nv, ns = per * nframes;
     std::vector<int64_t> soff(ns), slen(ns);
     int64_t base = 0;
     std::string err;
-    if (int rc = ffv1_slice_table(packets, frame_sizes, nframes, per, D->ec, soff.data(), slen.data(), &base, &err))
+    const bool carry_in = D->carry_valid;
+    D->carry_valid = false;  // until this decode has succeeded
+    if (int rc = ffv1_slice_table(packets, frame_sizes, nframes, per, R.ec, soff.data(), slen.data(), &base, &err))
         PP_FAIL(rc, "%s", err.c_str());
+    // GOPs: a keyframe starts one; frame 0 without one continues the previous decode's
+    std::vector<int> gop;
+    for (int f = 0; f < nframes; ++f) {
+        const int key = ffv1_keyframe_bit(packets + soff[(int64_t)f * per], slen[(int64_t)f * per]);
+        if (f == 0 || key) {
+            if (f == 0 && !key && !carry_in)
+                PP_FAIL(PP_ERR_INVALID, "frame 0 is not a keyframe and no earlier frame of its GOP was decoded");
+            gop.insert(gop.end(), {f, 0, key});
+        }
+        gop[gop.size() - 2]++;
+    }
+    const int ngops = (int)gop.size() / 3, nchains = ngops * per;
     if (base > D->pkt_cap) {
         if (D->pkt) PP_HIP(hipFree(D->pkt));
         D->pkt = nullptr;
@@ -569,9 +755,20 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     PP_HIP(hipMemcpyAsync(D->pkt, packets, base, hipMemcpyHostToDevice, st));
     PP_HIP(hipMemcpyAsync(D->soff, soff.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
     PP_HIP(hipMemcpyAsync(D->slen, slen.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
-    const int64_t sb = 2 * (int64_t)D->ctx_count * 16;  // one half, per slice
-    const size_t half = (size_t)sb * ((ns + 63) / 64 * 64);
-    PP_HIP(hipMemsetAsync(D->states, 128, 2 * half, st));
+    PP_HIP(hipMemcpyAsync(D->gop, gop.data(), sizeof(int) * gop.size(), hipMemcpyHostToDevice, st));
+    PP_HIP(hipMemsetAsync(D->status, 0, sizeof(int) * ns, st));
+    const int64_t sb = 2 * (int64_t)R.max_ctx * 16;  // one half, per chain
+    const int64_t half = sb * D->slots, used = sb * ((nchains + 63) / 64 * 64);
+    const int64_t chalf = sb * ((per + 63) / 64 * 64);
+    PP_HIP(hipMemsetAsync(D->states, 128, used, st));
+    PP_HIP(hipMemsetAsync(D->states + half, 128, used, st));
+    auto copy_states = [&](const uint8_t *src, int64_t sh, int s0, uint8_t *dstp, int64_t dh, int d0) {
+        const int64_t n = 2 * (int64_t)per * 2 * R.max_ctx;
+        hipLaunchKernelGGL(ffv1_state_copy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, sh, s0,
+                           dstp, dh, d0, per, 2 * R.max_ctx);
+        return hipGetLastError();
+    };
+    if (!gop[2]) PP_HIP(copy_states(D->carry, chalf, 0, D->states, half, 0));  // GOP 0 continues the carried states
     Ffv1DecArgs a{};
     a.pkt = D->pkt; a.soff = D->soff; a.slen = D->slen;
     for (int p = 0; p < 3; ++p) {
@@ -579,11 +776,18 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
         a.ls[p] = dst->linesize[p];
         a.fs[p] = dst->frame_stride[p];
     }
-    a.w = D->w; a.h = D->h; a.bytes = D->bits > 8 ? 2 : 1; a.bits = D->bits; a.hsub = D->hsub; a.vsub = D->vsub;
-    a.nh = D->nh; a.nv = D->nv; a.nslices = ns; a.ec = D->ec;
-    a.ctx_count = D->ctx_count; a.state_bytes = sb;
+    a.w = D->w; a.h = D->h; a.bytes = R.bits > 8 ? 2 : 1; a.bits = R.bits; a.hsub = R.hsub; a.vsub = R.vsub;
+    a.nh = R.nh; a.nv = R.nv; a.per = per; a.nchains = nchains; a.ec = R.ec; a.gop = D->gop;
+    a.max_ctx = R.max_ctx; a.ntables = R.ntables;
+    for (int t = 0; t < kFfv1MaxTables; ++t) {
+        a.ctx_count[t] = t < R.ntables ? R.ctx_count[t] : 0;
+        a.init_off[t] = t < R.ntables ? D->init_off[t] : -1;
+    }
+    a.state_bytes = sb;
     a.states = D->states; a.cold = D->states + half; a.status = D->status; a.tables = D->tables; a.quant = D->dquant;
-    a.lpw = D->lpw;
+    a.init = D->dinit;
+    // chains per workgroup: the LDS bound, spread over the CUs when chains are few (long GOPs)
+    a.lpw = std::max(1, std::min(D->lpw, (nchains + D->ctx->cus - 1) / std::max(1, D->ctx->cus)));
     if (const char *e = PP_KNOB("PIXPATH_FFV1_DEBUG")) a.debug = std::atoi(e);
     a.row_cap = D->row_cap;
     static const hipError_t attr = [] {
@@ -597,22 +801,25 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
         return hipSuccess;
     }();
     PP_HIP(attr);
-    const dim3 grid((ns + a.lpw - 1) / a.lpw), block(64);
-    const size_t lds = (size_t)a.lpw * D->row_cap * 2;
-    if (a.bytes == 2 && D->q0_alu)
+    const dim3 grid((nchains + a.lpw - 1) / a.lpw), block(64);
+    const size_t lds = (size_t)R.ntables * 5 * 256 * 2 + (size_t)a.lpw * D->row_cap * 2 * (D->pix ? 1 : 2);
+    if (a.bytes == 2 && D->pix)
         hipLaunchKernelGGL((ffv1_decode_kernel<2, true>), grid, block, lds, st, a);
     else if (a.bytes == 2)
         hipLaunchKernelGGL((ffv1_decode_kernel<2, false>), grid, block, lds, st, a);
-    else if (D->q0_alu)
+    else if (D->pix)
         hipLaunchKernelGGL((ffv1_decode_kernel<1, true>), grid, block, lds, st, a);
     else
         hipLaunchKernelGGL((ffv1_decode_kernel<1, false>), grid, block, lds, st, a);
     PP_HIP(hipGetLastError());
+    // the last GOP's states, for a next decode that continues it
+    PP_HIP(copy_states(D->states, half, (ngops - 1) * per, D->carry, chalf, 0));
     std::vector<int> status(ns);
     PP_HIP(hipMemcpyAsync(status.data(), D->status, sizeof(int) * ns, hipMemcpyDeviceToHost, st));
     PP_HIP(hipStreamSynchronize(st));
     static const char *what[] = {"ok", "slice CRC mismatch", "bad slice header", "bytestream end mismatch"};
     for (int i = 0; i < ns; ++i)
         if (status[i]) PP_FAIL(PP_ERR_INVALID, "frame %d slice %d: %s", i / per, i % per, what[std::min(status[i], 3)]);
+    D->carry_valid = true;
     return PP_OK;
 }

@@ -123,14 +123,23 @@ struct HostRD {
         return 1;
     }
     int symbol(uint8_t *st) {  // unsigned; -1 past 31 exponent bits (corrupt)
+        bool bad = false;
+        const int v = ssymbol(st, false, &bad);
+        return bad ? -1 : v;
+    }
+    // get_symbol (ffv1dec.c): sign at state 11 + min(e, 10); *bad past 30 exponent bits
+    int ssymbol(uint8_t *st, bool is_signed, bool *bad) {
         if (rac(st)) return 0;
         int e = 0;
         while (rac(st + 1 + std::min(e, 9))) {
-            if (++e > 30) return -1;
+            if (++e > 30) {
+                *bad = true;
+                return 0;
+            }
         }
         int a = 1;
         for (int i = e - 1; i >= 0; i--) a += a + rac(st + 22 + std::min(i, 9));
-        return a;
+        return is_signed && rac(st + 11 + std::min(e, 10)) ? -a : a;
     }
 };
 
@@ -231,12 +240,29 @@ int ffv1_parse_record(const uint8_t *extra, int size, int w, int h, Ffv1Record *
         if (crc) return fail(err, PP_ERR_INVALID, "configuration record CRC mismatch");
     }
     Ffv1Record R;
-    HostRD r(extra, size);
+    HostRD r(extra, size - 4);  // read_extra_header: the CRC is not range-coded data
     uint8_t st[kFfv1CtxBytes];
     std::memset(st, 128, sizeof(st));
+    bool bad = false;
     const int version = r.symbol(st);
-    const int micro = r.symbol(st);
-    const int coder = r.symbol(st);
+    R.micro = r.symbol(st);
+    R.coder = r.symbol(st);
+    if (version != 3 || R.micro < 0 || (R.coder != 1 && R.coder != 2))
+        return fail(err, PP_ERR_UNSUPPORTED, "FFV1 record: version %d coder %d (supported: version 3, range coder 1 or 2)",
+                    version, R.coder);
+    rac_states(R.zero_state, R.one_state);
+    if (R.coder == 2) {  // AC_RANGE_CUSTOM_TAB: state_transition[i] - one_state[i], signed
+        uint8_t one[256];
+        for (int i = 1; i < 256; i++) {
+            const int v = r.ssymbol(st, true, &bad) + r.one[i];
+            if (bad || v < 1 || v > 255) return fail(err, PP_ERR_INVALID, "FFV1 record: state transition %d", v);
+            one[i] = (uint8_t)v;
+        }
+        for (int i = 1; i < 256; i++) {  // ff_ffv1_init_slice_state
+            R.one_state[i] = one[i];
+            R.zero_state[256 - i] = (uint8_t)(256 - one[i]);
+        }
+    }
     const int cs = r.symbol(st);
     R.bits = r.symbol(st);
     const int chroma = r.rac(st);
@@ -244,13 +270,11 @@ int ffv1_parse_record(const uint8_t *extra, int size, int w, int h, Ffv1Record *
     R.vsub = r.symbol(st);
     const int alpha = r.rac(st);
     const int nh1 = r.symbol(st), nv1 = r.symbol(st);
-    const int tables = r.symbol(st);
-    (void)micro;
-    if (version != 3 || coder != 1 || cs != 0 || !chroma || alpha || tables != 1)
-        return fail(err, PP_ERR_UNSUPPORTED,
-                    "FFV1 record: version %d coder %d colorspace %d chroma %d alpha %d tables %d "
-                    "(supported: 3, 1, 0, 1, 0, 1)", version, coder, cs, chroma, alpha, tables);
-    if ((R.bits != 8 && R.bits != 10) || R.hsub != 1 || R.vsub < 0 || R.vsub > 1)
+    R.ntables = r.symbol(st);
+    if (cs != 0 || !chroma || alpha)
+        return fail(err, PP_ERR_UNSUPPORTED, "FFV1 record: colorspace %d chroma %d alpha %d (supported: YCbCr, chroma, no alpha)",
+                    cs, chroma, alpha);
+    if (R.bits < 8 || R.bits > 10 || R.hsub < 0 || R.hsub > 1 || R.vsub < 0 || R.vsub > 1)
         return fail(err, PP_ERR_UNSUPPORTED, "FFV1 record: %d bits, chroma shifts %d/%d", R.bits, R.hsub, R.vsub);
     if (nh1 < 0 || nv1 < 0 || nh1 >= 256 || nv1 >= 256)
         return fail(err, PP_ERR_INVALID, "FFV1 record: slice grid %dx%d", nh1 + 1, nv1 + 1);
@@ -258,35 +282,56 @@ int ffv1_parse_record(const uint8_t *extra, int size, int w, int h, Ffv1Record *
     R.nv = nv1 + 1;
     if (R.nh * R.nv > 256 || R.nh > w || R.nv > h)
         return fail(err, PP_ERR_INVALID, "FFV1 record: slice grid %dx%d", R.nh, R.nv);
-    // read_quant_tables: 5 run-length tables; only the first three may vary
-    int64_t cc = 1;
-    for (int t = 0; t < 5; t++) {
-        uint8_t qs[kFfv1CtxBytes];
-        std::memset(qs, 128, sizeof(qs));
-        int16_t q[256];
-        int i = 0, v = 0;
-        for (; i < 128; v++) {
-            const int run = r.symbol(qs);  // run length - 1
-            if (run < 0 || run >= 128 - i) return fail(err, PP_ERR_INVALID, "FFV1 record: quantisation table %d", t);
-            for (int k = 0; k <= run; k++) q[i++] = (int16_t)(cc * v);
+    if (R.ntables < 1 || R.ntables > kFfv1MaxTables)
+        return fail(err, PP_ERR_INVALID, "FFV1 record: %d quantisation table sets", R.ntables);
+    for (int s = 0; s < R.ntables; s++) {  // read_quant_tables
+        int64_t cc = 1;
+        for (int t = 0; t < 5; t++) {
+            uint8_t qs[kFfv1CtxBytes];
+            std::memset(qs, 128, sizeof(qs));
+            int16_t *q = R.quant[s][t];
+            int i = 0, v = 0;
+            for (; i < 128; v++) {
+                const int run = r.symbol(qs);  // run length - 1
+                if (run < 0 || run >= 128 - i)
+                    return fail(err, PP_ERR_INVALID, "FFV1 record: quantisation table %d.%d", s, t);
+                for (int k = 0; k <= run; k++) q[i++] = (int16_t)(cc * v);
+            }
+            for (i = 1; i < 128; i++) q[256 - i] = (int16_t)-q[i];
+            q[128] = (int16_t)-q[127];
+            cc *= 2 * v - 1;
+            if (cc > 32768) return fail(err, PP_ERR_INVALID, "FFV1 record: quantisation set %d: too many contexts", s);
         }
-        for (i = 1; i < 128; i++) q[256 - i] = (int16_t)-q[i];
-        q[128] = (int16_t)-q[127];
-        const int levels = 2 * v - 1;
-        if (t >= 3 && levels != 1) return fail(err, PP_ERR_UNSUPPORTED, "FFV1 record: 5-input context model");
-        if (t < 3) std::memcpy(R.quant[t], q, sizeof(q));
-        cc *= levels;
-        if (cc > 2 * kFfv1MaxCtx) return fail(err, PP_ERR_UNSUPPORTED, "FFV1 record: more than %d contexts", kFfv1MaxCtx);
+        R.ctx_count[s] = (int)((cc + 1) / 2);
+        R.max_ctx = std::max(R.max_ctx, R.ctx_count[s]);
     }
-    R.ctx_count = (int)((cc + 1) / 2);
-    if (R.ctx_count > kFfv1MaxCtx) return fail(err, PP_ERR_UNSUPPORTED, "FFV1 record: %d contexts", R.ctx_count);
-    if (r.rac(st)) return fail(err, PP_ERR_UNSUPPORTED, "FFV1 record: initial states");
+    uint8_t st2[kFfv1CtxBytes][kFfv1CtxBytes];
+    std::memset(st2, 128, sizeof(st2));
+    for (int s = 0; s < R.ntables; s++) {
+        if (!r.rac(st)) continue;
+        R.init[s].resize((size_t)R.ctx_count[s] * kFfv1CtxBytes);
+        uint8_t *p = R.init[s].data();
+        for (int j = 0; j < R.ctx_count[s]; j++)
+            for (int k = 0; k < kFfv1CtxBytes; k++) {
+                const int pred = j ? p[(j - 1) * kFfv1CtxBytes + k] : 128;
+                const int d = r.ssymbol(st2[k], true, &bad);
+                if (bad) return fail(err, PP_ERR_INVALID, "FFV1 record: initial states of set %d", s);
+                p[j * kFfv1CtxBytes + k] = (uint8_t)((pred + d) & 0xFF);
+            }
+    }
     R.ec = r.symbol(st);
     if (R.ec < 0 || R.ec > 1) return fail(err, PP_ERR_INVALID, "FFV1 record: ec %d", R.ec);
-    const int intra = r.symbol(st);
-    if (intra != 1) return fail(err, PP_ERR_UNSUPPORTED, "FFV1 record: inter frames (intra %d)", intra);
+    R.intra = R.micro > 2 ? r.symbol(st) : 0;
+    if (R.intra < 0) return fail(err, PP_ERR_INVALID, "FFV1 record: intra %d", R.intra);
     *rec = R;
     return PP_OK;
+}
+
+int ffv1_keyframe_bit(const uint8_t *slice0, int64_t n) {
+    // the first decision of the frame coder at state 128 (decode_frame):
+    // range 0xFF00 splits at 0x7F80; ff_init_range_decoder clamps low to 0xFF00
+    const int low = n >= 2 ? ((int)slice0[0] << 8) | slice0[1] : 0;
+    return std::min(low, 0xFF00) >= 0x7F80 ? 1 : 0;
 }
 
 int ffv1_slice_table(const uint8_t *packets, const int64_t *frame_sizes, int nframes, int per, int ec,

@@ -14,7 +14,8 @@ namespace pp {
 
 constexpr int kFfv1Ctx = 666;   // (11^3 + 1) / 2 contexts of the 3-input set the encoder writes
 constexpr int kFfv1CtxBytes = 32;  // state bytes per context
-constexpr int kFfv1MaxCtx = 4096;  // context count the decoder's state blocks are sized for
+constexpr int kFfv1MaxCtx = 16384; // (32768 + 1) / 2: read_quant_tables' bound on one set
+constexpr int kFfv1MaxTables = 8;  // MAX_QUANT_TABLES
 
 // ff_build_rac_states(c, 0.05 * 2^32, 256 - 8): the default state-transition table
 void rac_states(uint8_t zero[256], uint8_t one[256]);
@@ -28,15 +29,29 @@ int ffv1_quant(int i);
 // 3-input quantisation set, slice CRCs, intra; CRC-32 parity appended.
 std::vector<uint8_t> ffv1_write_record(int depth, int hsub, int vsub, int slices_h, int slices_v);
 
-// What the decoder needs from a configuration record.
+// What the decoder needs from a configuration record (RFC 9043 4.2,
+// ffv1dec.c read_extra_header): version 3, range coder with the default
+// (coder_type 1) or a transmitted (2) state-transition table, YCbCr with
+// chroma planes and no alpha, 8..10 bits, 4:2:0 / 4:2:2 / 4:4:4, up to 8
+// quantisation table sets of up to 5 inputs, optional initial context states
+// per set, slice CRCs or not, intra or inter.
 struct Ffv1Record {
-    int bits = 8, hsub = 1, vsub = 1, nh = 1, nv = 1, ec = 0, ctx_count = 0;
-    int16_t quant[3][256];
+    int bits = 8, hsub = 1, vsub = 1, nh = 1, nv = 1, ec = 0, intra = 1, micro = 0, coder = 1;
+    int ntables = 0;
+    int ctx_count[kFfv1MaxTables] = {};
+    int max_ctx = 0;                            // largest set: the decoder's per-plane state slots
+    int16_t quant[kFfv1MaxTables][5][256];      // scaled, mirrored (read_quant_tables)
+    uint8_t zero_state[256], one_state[256];    // the slice coders' table
+    std::vector<uint8_t> init[kFfv1MaxTables];  // [ctx_count][32] when transmitted, else empty (128s)
 };
 
 // Parse and check a configuration record for a w x h stream: 0 (PP_OK), or a
 // negative PP_ERR_* with *err set.  Never reads outside extra[0, size).
 int ffv1_parse_record(const uint8_t *extra, int size, int w, int h, Ffv1Record *rec, std::string *err);
+
+// The keyframe flag of a frame packet: the first range-coded decision of
+// its first slice (at state 128, before any table is involved).
+int ffv1_keyframe_bit(const uint8_t *slice0, int64_t n);
 
 // The slice table of `nframes` packets held back to back (frame_sizes[f]
 // bytes each): every frame's slice footers walked backwards from the packet

@@ -100,7 +100,8 @@ long fuzz_records(Rng &r, int iters) {
             std::vector<uint8_t> b = exact(rec);
             const int rc = ffv1_parse_record(b.data(), (int)b.size(), w, h, &out, &err);
             CHECK(rc == 0 && out.bits == f[0] && out.hsub == f[1] && out.vsub == f[2] && out.nh == nh &&
-                      out.nv == nv && out.ec == 1 && out.ctx_count == kFfv1Ctx,
+                      out.nv == nv && out.ec == 1 && out.ntables == 1 && out.ctx_count[0] == kFfv1Ctx && out.intra == 1 &&
+                      out.coder == 1,
                   "record %d/%d/%d %dx%d did not round trip: %d %s", f[0], f[1], f[2], nh, nv, rc, err.c_str());
         }
         std::vector<uint8_t> m = rec;

@@ -434,8 +434,15 @@ struct pp_scale_plan {
     int chain_out = 0;                // target bit depth
     Kind first_kind = GENERIC;        // the first stage's own kind (two-launch path)
     bool chain_fused = false;         // one strip_kernel launch does both stages
-    size_t chain_lds = 0;
+    size_t chain_lds = 0;             // the fused launch's LDS (with `luma`: the chroma launch's)
     void *dev2 = nullptr;             // second-stage tables (vrow2, chunk2)
+    // CHAIN, fused, 4:2:0 -> 4:2:2 target: luma's second stage is an identity
+    // bank, so luma runs as its own launch of this first-stage plan (config-2
+    // tiling: 32-row chunks, no second-stage ring) and the chain launch keeps
+    // the chroma planes only -- LDS is sized per launch, so luma no longer
+    // takes the 16-row chunks and ring2 LDS the chroma planes need
+    pp_scale_plan *luma = nullptr;
+    size_t fast_lds_plane[2] = {0, 0};  // strip_kernel LDS of the luma / chroma jobs alone
 };
 
 namespace {
@@ -764,7 +771,8 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
             for (int c = 0; c < 2 && HW > 0; ++c) {
                 fast_coefs(hp[c], c ? P->cdw : dw, HW);
                 hp[c].S_fast = std::max(hp[c].f_S, (hp[c].max_base + 2 * HW + 15) & ~15);
-                lds = std::max(lds, (size_t)hp[c].maxnew * hp[c].S_fast * 2 + (size_t)hp[c].ring * ftw * 2);
+                P->fast_lds_plane[c] = (size_t)hp[c].maxnew * hp[c].S_fast * 2 + (size_t)hp[c].ring * ftw * 2;
+                lds = std::max(lds, P->fast_lds_plane[c]);
             }
             if (HW > 0 && lds <= lds_budget() * (size_t)(ftw / 256)) {
                 P->fast_hw = HW;
@@ -895,6 +903,10 @@ bool identity_bank(const pp::FilterBank &f, int one) {
 #define PIXPATH_CHAIN_CHO 16
 #endif
 constexpr int kChainCho = PIXPATH_CHAIN_CHO;
+#ifndef PIXPATH_CHAIN_SEG2
+#define PIXPATH_CHAIN_SEG2 4
+#endif
+constexpr int kChainSeg2 = PIXPATH_CHAIN_SEG2;  // second-stage segments of a chain plan's chroma planes
 
 // create_avpvs_segment's two stages (lib/ffmpeg.py:1037-1048): the scale
 // filter writes the overlay's yuv420p (overlay's default format=yuv420), then
@@ -937,7 +949,7 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
     bool ok = p2->kind == pp_scale_plan::COPY ||
               (identity_bank(p2->f[0], 1 << 14) && identity_bank(p2->f[1], 1 << 14) &&
                identity_bank(p2->f[2], 1 << 12) && (v422 || identity_bank(p2->f[3], 1 << 12)));
-    std::vector<int32_t> vrow2, chunk2;
+    std::vector<int32_t> vrow2, chunk2, seg2;
     int vtp2 = 0, ring2 = 0;
     if (ok && v422) {
         // second-stage chroma rows: compact window, tap pairs, record per row
@@ -977,31 +989,56 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
             ring2 = std::max(ring2, top - b2);
         }
         ring2 = (ring2 + 1) & ~1;
+        // segments of the second-stage rows (the first stage's chroma walk is
+        // one segment so that the second stage's taps are always in ring2):
+        // each segment's walk starts at the chunk of its first row's window
+        // and ends at the chunk that completes its last row, recomputing the
+        // few first-stage rows of the halo instead of one 1080-row workgroup
+        // per strip (4,800 long workgroups per 600-frame launch: a tail)
+        int nseg2 = kChainSeg2;
+        if (const char *e = PP_KNOB("PIXPATH_CHAIN_SEG2")) nseg2 = std::max(1, atoi(e));
+        nseg2 = std::min(nseg2, std::max(1, dh2 / 16));
+        seg2.assign((size_t)nseg2 * 4, 0);
+        for (int sg = 0; sg < nseg2; ++sg) {
+            const int r0 = (int)((int64_t)sg * dh2 / nseg2), r1 = (int)((int64_t)(sg + 1) * dh2 / nseg2);
+            seg2[4 * sg] = h2.vbase[r0] / cho * cho;
+            seg2[4 * sg + 1] = std::min(cdh1, (need[r1 - 1] / cho + 1) * cho);
+            seg2[4 * sg + 2] = r0;
+            seg2[4 * sg + 3] = r1;
+        }
     }
-#ifdef PIXPATH_RING2_WORDS
-    const size_t lds = P->fast_lds + (size_t)ring2 * P->fast_tw * 2;
-    const int r2rows = ring2;
-#else
     // the byte ring is circular: a power of two of rows >= every chunk's live span
     int r2rows = 2;
     while (r2rows < ring2) r2rows <<= 1;
     const size_t lds = P->fast_lds + (ring2 ? (size_t)r2rows * P->fast_tw : 0);
-#endif
     if (!ok || lds > 64 * 1024) {
         *out = P.release();
         return PP_OK;
     }
+    // luma as its own launch (4:2:2 targets: the chroma launch then carries
+    // only the ring2 planes): its plan is the plain first stage, same filters
+    pp_scale_plan *lp = nullptr;
+    if (v422 && plan_create(ctx, src_fmt, sw, sh, PP_FMT_YUV420P, dw, dh, flags, p0, p1, false, &lp) == PP_OK) {
+        if (lp->kind == pp_scale_plan::GENERIC && lp->fast_hw > 0 && lp->fast_tw == 256) {
+            P->luma = lp;
+            lp->fjob[0].fuse = P->chain_out > 8 ? 1 : 0;
+        } else {
+            (void)pp_scale_plan_destroy(lp);
+        }
+    }
+    const size_t chain_lds = P->luma ? P->fast_lds_plane[1] + (size_t)r2rows * P->fast_tw : lds;
     if (!ctx) {  // host-only plan: introspection (pp_scale_plan_path / _stats) only
         P->chain_fused = true;
-        P->chain_lds = lds;
+        P->chain_lds = chain_lds;
         *out = P.release();
         return PP_OK;
     }
-    const size_t b1 = (vrow2.size() * 4 + 255) & ~size_t(255), b2 = chunk2.size() * 4;
+    const size_t b1 = (vrow2.size() * 4 + 255) & ~size_t(255), b2 = (chunk2.size() * 4 + 255) & ~size_t(255);
     if (v422) {
-        PP_HIP(hipMalloc(&P->dev2, b1 + b2));
+        PP_HIP(hipMalloc(&P->dev2, b1 + b2 + seg2.size() * 4));
         PP_HIP(hipMemcpy(P->dev2, vrow2.data(), vrow2.size() * 4, hipMemcpyHostToDevice));
-        PP_HIP(hipMemcpy(static_cast<uint8_t *>(P->dev2) + b1, chunk2.data(), b2, hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(static_cast<uint8_t *>(P->dev2) + b1, chunk2.data(), chunk2.size() * 4, hipMemcpyHostToDevice));
+        PP_HIP(hipMemcpy(static_cast<uint8_t *>(P->dev2) + b1 + b2, seg2.data(), seg2.size() * 4, hipMemcpyHostToDevice));
     }
     const int widen = P->chain_out > 8 ? 1 : 0;
     for (int p = 0; p < 3; ++p) {
@@ -1012,10 +1049,12 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
             J.r2mask = r2rows - 1;
             J.vrow2 = static_cast<const int32_t *>(P->dev2);
             J.chunk2 = reinterpret_cast<const int32_t *>(static_cast<uint8_t *>(P->dev2) + b1);
+            J.seg2 = reinterpret_cast<const int32_t *>(static_cast<uint8_t *>(P->dev2) + b1 + b2);
+            J.tiles_y = (int)seg2.size() / 4;
         }
     }
     P->chain_fused = true;
-    P->chain_lds = lds;
+    P->chain_lds = chain_lds;
     *out = P.release();
     return PP_OK;
 }
@@ -1023,6 +1062,7 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
 extern "C" int pp_scale_plan_destroy(pp_scale_plan *P) {
     if (!P) return PP_OK;
     if (P->stage2) (void)pp_scale_plan_destroy(P->stage2);
+    if (P->luma) (void)pp_scale_plan_destroy(P->luma);
     if (P->dev2) (void)hipFree(P->dev2);
     if (P->dev) (void)hipFree(P->dev);
     if (P->scratch) (void)hipFree(P->scratch);
@@ -1165,45 +1205,70 @@ int launch_packed(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, 
     return PP_OK;
 }
 
-// CHAIN, fused: one strip_kernel<.., FUSE = target depth> launch
-int launch_chain(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, int nframes, hipStream_t st) {
+// CHAIN, fused: strip_kernel<.., FUSE = target depth> launches over the
+// planes `pl` (job, source / destination plane index), tile bases renumbered
+// for the launch
+int launch_chain_planes(pp_scale_plan *P, const pp::PlaneJob *const *jobs, const int *pl, int np, int hw, size_t lds,
+                        const pp_frames *src, const pp_frames *dst, int nframes, hipStream_t st) {
     using namespace pp;
     ScaleArgs a{};
-    a.nplanes = 3;
-    for (int p = 0; p < 3; ++p) {
-        a.pl[p] = P->fjob[p];
-        a.src[p] = static_cast<const uint8_t *>(src->data[p]);
-        a.sls[p] = src->linesize[p];
-        a.sfs[p] = src->frame_stride[p];
-        a.dst[p] = static_cast<uint8_t *>(dst->data[p]);
-        a.dls[p] = dst->linesize[p];
-        a.dfs[p] = dst->frame_stride[p];
+    a.nplanes = np;
+    int tiles = 0, vtp = 1;
+    for (int i = 0; i < np; ++i) {
+        const int p = pl[i];
+        a.pl[i] = *jobs[i];
+        a.pl[i].tile_base = tiles;
+        tiles += a.pl[i].tiles_x * a.pl[i].tiles_y;
+        vtp = std::max(vtp, a.pl[i].vtp);
+        a.src[i] = static_cast<const uint8_t *>(src->data[p]);
+        a.sls[i] = src->linesize[p];
+        a.sfs[i] = src->frame_stride[p];
+        a.dst[i] = static_cast<uint8_t *>(dst->data[p]);
+        a.dls[i] = dst->linesize[p];
+        a.dfs[i] = dst->frame_stride[p];
     }
     a.hshift = P->si.depth == 8 ? 7 : P->si.depth - 1;
     a.dither = P->si.depth > 8;
     a.vec_src = 1;
     a.vec_dst = 1;
     if (const char *e = PP_KNOB("PIXPATH_SCALE_DEBUG")) a.debug = atoi(e);
-    for (int p = 0; p < 3; ++p)
-        a.vec_dst &= aligned(a.dst[p], a.dls[p], nframes > 1 ? a.dfs[p] : 0, P->chain_out == 8 ? 4 : 8);
-    const int vtm = strip_vtm_bucket(std::max(P->fjob[0].vtp, P->fjob[1].vtp));
-    KernelFn k = P->si.depth == 8 ? pick_strip_chain_u8(P->chain_out, P->fast_hw, vtm)
-                                  : pick_strip_chain_u16(P->chain_out, P->fast_hw, vtm);
-    if (!k) PP_FAIL(PP_ERR_UNSUPPORTED, "no chain kernel for window %d", P->fast_hw);
-    const int tiles = P->fast_tiles;
+    for (int i = 0; i < np; ++i)
+        a.vec_dst &= aligned(a.dst[i], a.dls[i], nframes > 1 ? a.dfs[i] : 0, P->chain_out == 8 ? 4 : 8);
+    const int vtm = strip_vtm_bucket(vtp);
+    KernelFn k = P->si.depth == 8 ? pick_strip_chain_u8(P->chain_out, hw, vtm) : pick_strip_chain_u16(P->chain_out, hw, vtm);
+    if (!k) PP_FAIL(PP_ERR_UNSUPPORTED, "no chain kernel for window %d", hw);
     a.tiles = tiles;
     const int fmax = std::max(1, (1 << 30) / tiles);
     for (int f0 = 0; f0 < nframes; f0 += fmax) {
         const int nf = std::min(fmax, nframes - f0);
         ScaleArgs b = a;
-        for (int p = 0; p < 3; ++p) {
-            b.src[p] += f0 * a.sfs[p];
-            b.dst[p] += f0 * a.dfs[p];
+        for (int i = 0; i < np; ++i) {
+            b.src[i] += f0 * a.sfs[i];
+            b.dst[i] += f0 * a.dfs[i];
         }
-        hipLaunchKernelGGL(k, dim3(tiles * nf), dim3(kThreads), P->chain_lds, st, b);
+        hipLaunchKernelGGL(k, dim3(tiles * nf), dim3(kThreads), lds, st, b);
     }
     PP_HIP(hipGetLastError());
     return PP_OK;
+}
+
+// CHAIN, fused: one launch over all planes, or (P->luma) the luma launch of
+// the plain first-stage plan, then the chroma planes' chain launch
+int launch_chain(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, int nframes, hipStream_t st) {
+    using namespace pp;
+    if (P->luma) {
+        const PlaneJob *lj[1] = {&P->luma->fjob[0]};
+        const int lpl[1] = {0};
+        if (int rc = launch_chain_planes(P, lj, lpl, 1, P->luma->fast_hw, P->luma->fast_lds_plane[0], src, dst,
+                                         nframes, st))
+            return rc;
+        const PlaneJob *cj[2] = {&P->fjob[1], &P->fjob[2]};
+        const int cpl[2] = {1, 2};
+        return launch_chain_planes(P, cj, cpl, 2, P->fast_hw, P->chain_lds, src, dst, nframes, st);
+    }
+    const PlaneJob *jobs[3] = {&P->fjob[0], &P->fjob[1], &P->fjob[2]};
+    const int pl[3] = {0, 1, 2};
+    return launch_chain_planes(P, jobs, pl, 3, P->fast_hw, P->chain_lds, src, dst, nframes, st);
 }
 
 }  // namespace

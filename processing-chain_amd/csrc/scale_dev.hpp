@@ -73,6 +73,8 @@ struct PlaneJob {
     int r2mask;             // fuse 2: rows of the circular byte ring2 - 1 (a power of two)
     const int32_t *vrow2;   // [dh2][16] second-stage row records (base row, tap pairs)
     const int32_t *chunk2;  // [nch][4] per chunk: second-stage rows [lo2, hi2), ring2 base row, kept pairs
+    const int32_t *seg2;    // fuse 2: [tiles_y][4] per segment: first-stage rows [y0, y1) (chunk aligned,
+                            // overlapping by the second stage's halo), second-stage rows [r0, r1) it stores
     int pk_off, pk_step;    // strip_kernel FUSE == 1: byte offset / step of this plane in the uyvy422 row
 };
 

@@ -133,9 +133,6 @@ constexpr int strip_chain_min_waves() {
 // windows, chain plans with 10+ dword windows spilled 1-5 VGPRs with it).
 template <typename ST, int OUTB, int HW, int VTM, int FUSE>
 constexpr bool strip_clamp_path() {
-#ifdef PIXPATH_NO_CLAMP_PLAIN
-    if (FUSE == 0) return false;
-#endif
     return !(FUSE >= 8 && HW >= 10) && !(sizeof(ST) == 1 && OUTB == 8 && HW == 4 && (FUSE >= 8 || VTM >= 5));
 }
 
@@ -165,14 +162,10 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
     const int cx = (tid & (TW / 4 - 1)) * 4;
     uint16_t *src_t = lds;                                                  // [maxnew][S]
     uint32_t *win = reinterpret_cast<uint32_t *>(lds + J.maxnew * S);       // [ring/2][TW] row pairs
-#ifdef PIXPATH_RING2_WORDS
-    uint32_t *ring2 = win + (J.ring >> 1) * TW;                             // FUSE, fuse 2: [ring2/2][TW]
-#else
     // FUSE, fuse 2: the second stage's input rows as bytes, a circular ring of
     // J.r2mask + 1 rows ([row & r2mask][TW] bytes): a lane stores its 4 bytes
     // of a row in one conflict-free dword, and no row is ever moved
     uint8_t *ring2b = reinterpret_cast<uint8_t *>(win + (J.ring >> 1) * TW);
-#endif
     const kconst int32_t *chunk2 = as_kconst<int32_t>(J.chunk2);            // [nch][4]: lo2, hi2, base2, keep2
     const ST *sbase = reinterpret_cast<const ST *>(a.src[p] + frame * a.sfs[p]);
     uint8_t *dbase = a.dst[p] + frame * a.dfs[p];
@@ -253,7 +246,17 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
         }
     };
 
-    const int y_begin = seg * J.seg_h, y_end = min(J.dh, y_begin + J.seg_h);
+    int y_begin = seg * J.seg_h, y_end = min(J.dh, y_begin + J.seg_h);
+    int r2lo = 0, r2hi = 0;  // fuse 2: the second-stage rows this segment stores
+    if constexpr (FUSE >= 8) {
+        if (J.fuse == 2) {  // first-stage rows of the segment plus the halo its second-stage rows read
+            const kconst int32_t *sg = as_kconst<int32_t>(J.seg2) + 4 * seg;
+            y_begin = sg[0];
+            y_end = sg[1];
+            r2lo = sg[2];
+            r2hi = sg[3];
+        }
+    }
     const int cho = J.cho;
     int next_src = chunk_lo[y_begin / cho];
     int base = next_src & ~1;
@@ -303,19 +306,6 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
             for (int k = 0; k < keep; ++k) win[k * TW + tid] = win[(k + shift) * TW + tid];
             moved = true;
         }
-#ifdef PIXPATH_RING2_WORDS
-        int base2 = 0;
-        if constexpr (FUSE >= 8) {
-            if (J.fuse == 2) {  // ring2 keeps the rows the pending second-stage outputs still read
-                base2 = chunk2[4 * ci + 2];
-                const int shift2 = ci ? (base2 - chunk2[4 * ci - 2]) >> 1 : 0, keep2 = chunk2[4 * ci + 3];
-                if (shift2 > 0) {
-                    for (int k = 0; k < keep2; ++k) ring2[k * TW + tid] = ring2[(k + shift2) * TW + tid];
-                    moved = true;
-                }
-            }
-        }
-#endif
         if (moved) __syncthreads();
         base = nbase;
         // ---- horizontal pass: row pairs of the window, wave-strided ----------
@@ -356,9 +346,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
         // ---- vertical pass: one output row per wave --------------------------
         // raised priority while the wave issues its output rows: the other
         // waves' H pass never starves the write stream (-2 %, profiles/r2)
-#ifndef PIXPATH_NO_SETPRIO
         __builtin_amdgcn_s_setprio(1);
-#endif
         const int ny = min(cho, y_end - y0);
         // VT (= vtp) tap pairs, compile-time per instance: every window read of
         // a row is in flight before the first v_dot2 waits on one
@@ -369,11 +357,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
             // row records (window base row + VT tap pairs) of G rows at a time
             // through the scalar cache: one exposed scalar-load latency per
             // group, not per row (the ds_reads of a row depend on its base)
-#ifdef PIXPATH_VPASS_G8
-            constexpr int G = VT <= 5 ? 8 : 4;
-#else
             constexpr int G = VT <= 2 ? 8 : VT <= 5 ? 4 : 2;
-#endif
             for (int g0 = rg; g0 < ny; g0 += 4 * G) {
                 int vb[G];
                 int32_t cf[G][VT];
@@ -427,11 +411,6 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                     for (int j = 0; j < 4; ++j) o[j] = min(max(acc[j] >> sh, 0), mx);
                     if constexpr (FUSE >= 8) {
                         if (jfuse == 2) {  // into ring2 (second-stage input)
-#ifdef PIXPATH_RING2_WORDS
-                            uint16_t *r16 = reinterpret_cast<uint16_t *>(ring2 + ((y - base2) >> 1) * TW + vx);
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) r16[2 * j + (y & 1)] = static_cast<uint16_t>(o[j] << 7);
-#else
                             uint32_t bq[4];
 #pragma unroll
                             for (int j = 0; j < 4; ++j) {  // opaque bytes (v_ashr_pk_u8_i32, see store4)
@@ -440,7 +419,6 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                             }
                             *reinterpret_cast<uint32_t *>(ring2b + (y & J.r2mask) * TW + vx) =
                                 bq[0] | (bq[1] << 8) | (bq[2] << 16) | (bq[3] << 24);
-#endif
                             __builtin_amdgcn_sched_barrier(0);
                             continue;
                         }
@@ -491,7 +469,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
             // ---- second stage (fuse 2): vertical filter of the ring2 rows ----
             if (jfuse == 2 && !(PP_ABLATE(a.debug) & 16)) {  // debug 16: no second stage (timing only)
                 __syncthreads();  // this chunk's first-stage rows are in ring2
-                const int lo2 = chunk2[4 * ci], hi2 = chunk2[4 * ci + 1];
+                const int lo2 = max(chunk2[4 * ci], r2lo), hi2 = min(chunk2[4 * ci + 1], r2hi);
                 const kconst int32_t *vrow2 = as_kconst<int32_t>(J.vrow2);
                 // VT2 tap pairs compile-time; the row records of G2 rows come
                 // through the scalar cache at once (as in the first stage's V
@@ -516,14 +494,6 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                             const int r2 = g0 + 4 * i;
                             if (r2 >= hi2) break;
                             int acc[4];
-#ifdef PIXPATH_RING2_WORDS
-                            const uint4 *rp = reinterpret_cast<const uint4 *>(ring2 + ((vb[i] - base2) >> 1) * TW + vx);
-                            uint4 q[VT2];
-#pragma unroll
-                            for (int j = 0; j < VT2; ++j) q[j] = rp[j * (TW / 4)];
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) acc[j] = FUSE == 8 ? 64 << 12 : 1 << (10 + 16 - FUSE);
-#else
                             // rows vb + 2j, vb + 2j + 1 from the byte ring, interleaved into
                             // the (row, row + 1) sample pairs of v_dot2; the first stage's
                             // << 7 (hScale8To15 of the identity H filter) moves onto the sum
@@ -543,7 +513,6 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                             }
 #pragma unroll
                             for (int j = 0; j < 4; ++j) acc[j] = 0;
-#endif
 #pragma unroll
                             for (int j = 0; j < VT2; ++j) {
                                 const v2i16 c2 = __builtin_bit_cast(v2i16, cf[i][j]);
@@ -552,10 +521,8 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                                 acc[2] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].z), c2, acc[2], false);
                                 acc[3] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].w), c2, acc[3], false);
                             }
-#ifndef PIXPATH_RING2_WORDS
 #pragma unroll
                             for (int j = 0; j < 4; ++j) acc[j] = (acc[j] << 7) + (FUSE == 8 ? 64 << 12 : 1 << (10 + 16 - FUSE));
-#endif
                             if (!CL && !lane_any) continue;
                             constexpr int s2 = FUSE == 8 ? 19 : 11 + 16 - FUSE;
                             int w[4];

@@ -25,6 +25,7 @@ EXPORTS = (
     "pp_ffv1_encoder_create", "pp_ffv1_encoder_destroy", "pp_ffv1_extradata", "pp_ffv1_encode",
     "pp_ffv1_encode_packets", "pp_ffv1_encode_stats", "pp_ffv1_encoder_memory", "pp_ffv1_encoder_reserve",
     "pp_ffv1_decoder_create", "pp_ffv1_decoder_destroy", "pp_ffv1_decoder_format", "pp_ffv1_decoder_slices", "pp_ffv1_decode",
+    "pp_ffv1_decoder_geometry", "pp_ffv1_decoder_info", "pp_ffv1_decoder_reset",
 )
 PP_COPY_H2D, PP_COPY_D2H, PP_COPY_D2D = 1, 2, 3
 PP_NAL_H264, PP_NAL_H265 = 1, 2
@@ -113,6 +114,9 @@ def lib():
         "pp_ffv1_decoder_format": (i32, [vp]),
         "pp_ffv1_decoder_slices": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "pp_ffv1_decode": (i32, [vp, vp, vp, i32, fr, vp]),
+        "pp_ffv1_decoder_geometry": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
+        "pp_ffv1_decoder_info": (i32, [vp, vp, i32]),
+        "pp_ffv1_decoder_reset": (i32, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -161,6 +161,14 @@ def acquire_encoder(fmt, w, h, slices=(8, 8), max_frames=600, device=None):
     return Ffv1Encoder(fmt, w, h, slices=slices, max_frames=max_frames, device=device)
 
 
+def take_idle_encoder(fmt, w, h, slices=(8, 8), max_frames=600, device=None):
+    """An idle pooled encoder of this geometry, or None (nothing is allocated)."""
+    key = _pool_key(fmt, w, h, slices, max_frames, context(device).device)
+    with _POOL_LOCK:
+        idle = _POOL.get(key)
+        return idle.pop() if idle else None
+
+
 def release_encoder(enc, ok=True):
     """Return an encoder from acquire_encoder() to the pool; one that failed
     mid-encode (ok=False) is freed instead."""
@@ -208,9 +216,13 @@ def clear_pool():
 
 
 class Ffv1Decoder:
-    """FFV1 v3 intra decoder on the GPU (one lane per slice): the AVPVS read
-    back for the CPVS stage.  ``decode(packets, sizes)`` takes the frame
-    packets back to back in host memory and returns a FrameBatch in HBM."""
+    """FFV1 v3 decoder on the GPU (one lane per slice and GOP): the AVPVS read
+    back for the CPVS stage -- pixpath's intra streams and FFmpeg's
+    `-level 3 -coder 1 -context 1` ones (transmitted state table, 5-input
+    context sets, GOPs with carried states).  ``decode(packets, sizes)`` takes
+    consecutive frame packets back to back in host memory and returns a
+    FrameBatch in HBM; a call that starts inside a GOP continues the previous
+    call's states (``reset()`` after a seek)."""
 
     def __init__(self, extradata, w, h, max_frames=600, device=None, host_only=False):
         self.w, self.h, self.max_frames = int(w), int(h), int(max_frames)
@@ -225,6 +237,17 @@ class Ffv1Decoder:
         nh, nv = ctypes.c_int(), ctypes.c_int()
         check(lib().pp_ffv1_decoder_slices(h_, ctypes.byref(nh), ctypes.byref(nv)))
         self.slices = (nh.value, nv.value)
+        lpw, cap = ctypes.c_int(), ctypes.c_int()
+        check(lib().pp_ffv1_decoder_geometry(h_, ctypes.byref(lpw), ctypes.byref(cap)))
+        self.slices_per_workgroup, self.row_cap = lpw.value, cap.value
+        info = (ctypes.c_int * 8)()
+        n = check(lib().pp_ffv1_decoder_info(h_, info, 8))
+        self.info = dict(zip(("micro_version", "coder_type", "quant_table_sets", "max_contexts", "intra", "ec",
+                              "initial_states_mask", "pixpath_tables"), list(info)[:n]))
+
+    def reset(self):
+        """Forget the carried GOP states (the next decode must start at a keyframe)."""
+        check(lib().pp_ffv1_decoder_reset(self.handle))
 
     def __del__(self):
         if getattr(self, "handle", None):
@@ -252,7 +275,7 @@ class Ffv1Decoder:
 
 
 _DEV_LOCK = threading.Lock()
-_DEV_STATE = {}  # device index -> (encode lock, encode stream, host-upload stream)
+_DEV_STATE = {}  # device index -> (encode lock, encode stream, host-upload stream, packet D2H stream)
 
 
 def _device_state(device):
@@ -265,8 +288,9 @@ def _device_state(device):
     with _DEV_LOCK:
         st = _DEV_STATE.get(device)
         if st is None:
-            st = _DEV_STATE[device] = (threading.Lock(), torch.cuda.Stream(torch.device("cuda", device)),
-                                       torch.cuda.Stream(torch.device("cuda", device)))
+            dev = torch.device("cuda", device)
+            st = _DEV_STATE[device] = (threading.Lock(), torch.cuda.Stream(dev), torch.cuda.Stream(dev),
+                                       torch.cuda.Stream(dev))
         return st
 
 
@@ -316,11 +340,12 @@ class Ffv1AviWriter:
         self.cur, self.fill = 0, 0
         self.free[0].clear()
         if shared:
-            self.lock, self.stream, self.put_stream = _device_state(self.device.index)
+            self.lock, self.stream, self.put_stream, self.d2h_stream = _device_state(self.device.index)
         else:
             self.lock = threading.Lock()
             self.stream = torch.cuda.Stream(self.device)
             self.put_stream = torch.cuda.Stream(self.device)  # host-frame uploads
+            self.d2h_stream = torch.cuda.Stream(self.device)  # packet D2H
         self.avi = avi.AviWriter(path, w, h, rate, extradata=self.enc.extradata,
                                  info={b"ISFT": provenance(self.enc.slices).encode()})
         self.frames = 0
@@ -349,7 +374,12 @@ class Ffv1AviWriter:
                 return
             slot, n, ev, t_q = item
             try:
-                if not self.err:
+                if self.err:
+                    # after a failure: still wait for this batch's copies into the
+                    # staging batch (queued on the caller's stream) before close()
+                    # drops the stages back to the allocator
+                    ev.synchronize()
+                else:
                     t_w = time.perf_counter()
                     self.stream.wait_event(ev)
                     ev.synchronize()  # the frames of this batch are in the staging batch
@@ -359,9 +389,12 @@ class Ffv1AviWriter:
                         t0 = time.perf_counter()
                         with torch.cuda.stream(self.stream):
                             ptr, n, sizes = self.enc.encode_packets(src, stream=self.stream)
-                    # the packets leave on the copy stream, outside the lock: the
-                    # next writer's encode starts while this D2H runs
-                    data = self.enc.packets_to_host(ptr, n, self.put_stream)
+                    # the packets leave on the D2H stream, outside the lock: the next
+                    # writer's encode starts while this D2H runs, and no writer's host
+                    # upload (put_stream, synchronised per upload) waits behind it
+                    # (ADVICE r4); the D2H waits for the encode on its stream
+                    self.d2h_stream.wait_stream(self.stream)
+                    data = self.enc.packets_to_host(ptr, n, self.d2h_stream)
                     t1 = time.perf_counter()
                     self.avi.write_packets(data, sizes)
                     t2 = time.perf_counter()
@@ -469,6 +502,10 @@ class Ffv1AviWriter:
         finally:
             if not ok:
                 self.avi.abort()
+                try:  # copies into the staging batch still queued on the caller's stream
+                    self.last_stream.synchronize()
+                except Exception:
+                    pass
             self.release(ok)
 
 
@@ -602,16 +639,32 @@ def is_pixpath_ffv1(info):
     return probe.extradata == info["extradata"]
 
 
+def gpu_decodable(info):
+    """True when the GPU decoder reads an AVI's video stream (avi.scan info):
+    FFV1 whose configuration record pp_ffv1_decoder_create accepts -- pixpath's
+    own, and FFmpeg's `-level 3 -coder 1 -context 1 -slicecrc 1` AVPVS
+    (lib/ffmpeg.py:993, :1047) with its custom state table, 5-input contexts
+    and GOPs, at 8 or 10 bits, 4:2:0 / 4:2:2 / 4:4:4."""
+    from ._native import PixpathError
+    if info.get("fourcc") != b"FFV1" or not info.get("extradata") or "w" not in info:
+        return False
+    try:
+        Ffv1Decoder(info["extradata"], info["w"], info["h"], max_frames=1, host_only=True)
+    except (PixpathError, ValueError):
+        return False
+    return True
+
+
 def open_avpvs_reader(path, device=None, batch=600):
-    """The reader of an AVPVS: the GPU FFV1 decoder (Ffv1AviReader) for an AVI
-    pixpath's encoder wrote, else ffmpeg's decoder through pixpath.io (an
-    AVPVS from the reference, from a PIXPATH_FFV1=ffmpeg run, or one kept by
-    the `-n` skip rule)."""
+    """The reader of an AVPVS: the GPU FFV1 decoder (Ffv1AviReader) for an
+    FFV1 AVI it reads -- pixpath's, or the reference's own ffmpeg-made AVPVS --
+    else ffmpeg's decoder through pixpath.io (another codec, or a record the
+    GPU decoder refuses)."""
     from . import avi, io as pio
     scanned = None
     if path.lower().endswith(".avi") and os.path.isfile(path):
         scanned = avi.scan(path)
-        if is_pixpath_ffv1(scanned[0]):
+        if gpu_decodable(scanned[0]):
             return Ffv1AviReader(path, batch=batch, device=device, scanned=scanned)
     return pio.open_reader(path)
 
@@ -654,10 +707,16 @@ def stall_avi(src_path, dst_path, buffer_events, skipping, spinner_path=None, bl
                 pk = packet(s)
                 dec.decode(pk, [len(pk)], dst=FrameBatch.interleaved(dec.fmt, w, h, 1, device=dev,
                                                                       storage=sb.storage[k:k + 1]))
-            # the process's pooled 600-frame encoder (the AVPVS writer's, when the
-            # stall pass follows it in the same process) and its staging batch
-            B = 600
-            enc = acquire_encoder(dec.fmt, w, h, slices=dec.slices, max_frames=B, device=dev.index)
+            # the process's idle pooled 600-frame encoder (the AVPVS writer's, when
+            # the stall pass follows it in the same process) and its staging
+            # batch; else an encoder sized to the stall frames (a `cli stall`
+            # process composes a handful: ~22 GB for 600 frames would be wasted)
+            enc = take_idle_encoder(dec.fmt, w, h, slices=dec.slices, max_frames=600, device=dev.index)
+            pooled = enc is not None
+            if not pooled:
+                enc = Ffv1Encoder(dec.fmt, w, h, slices=dec.slices, max_frames=min(600, len(compose)),
+                                  device=dev.index)
+            B = enc.max_frames
             ok = False
             try:
                 if not enc.stages:
@@ -676,7 +735,8 @@ def stall_avi(src_path, dst_path, buffer_events, skipping, spinner_path=None, bl
                         o += k
                 ok = True
             finally:
-                release_encoder(enc, ok=ok)
+                if pooled:
+                    release_encoder(enc, ok=ok)
         wr = avi.AviWriter(dst_path, w, h, rate, extradata=info["extradata"],
                            info={b"ISFT": provenance(dec.slices).encode()})
         try:

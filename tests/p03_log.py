@@ -10,7 +10,7 @@ PIXPATH_FFV1=ffmpeg the reference's own `-c:v ffv1 ... -coder 1 -context 1
 -slicecrc 1` options.  The AVI itself carries the same tag (RIFF INFO ISFT,
 pixpath.ffv1.provenance).
 
-p03_log_line restates that line for tests and tools.
+p03_log_line restates that line for the tests (test helper, not product code).
 """
 
 

@@ -212,11 +212,17 @@ def test_ffv1_writer_slice_grid_setting(monkeypatch):
 
 
 def test_pixpath_ffv1_detection_and_reader_fallback(tmp_path, monkeypatch):
-    """Only AVIs whose FFV1 configuration record is exactly pixpath's encoder's
-    (for their format, size and slice grid) go to the GPU decoder; anything
-    else (FFmpeg's `-coder 1 -context 1` record, a corrupt record, another
-    codec) falls back to ffmpeg's decoder through pixpath.io."""
+    """is_pixpath_ffv1 (the packet-level stall's test) holds only for records
+    exactly pixpath's encoder's; the GPU decoder (open_avpvs_reader) also
+    takes FFmpeg's `-coder 1 -context 1` records (gpu_decodable); a corrupt
+    record or another codec falls back to ffmpeg's decoder through
+    pixpath.io."""
+    import ffv1_ref as ref
     from pixpath import avi, ffv1, io as pio
+    gen = ref.gen_extradata(ref.make_prof(10, 1, 0, 2, 2, ref.ffmpeg_context1_sets(10)))
+    assert not ffv1.is_pixpath_ffv1({"fourcc": b"FFV1", "w": 640, "h": 360, "extradata": gen})
+    assert ffv1.gpu_decodable({"fourcc": b"FFV1", "w": 640, "h": 360, "extradata": gen})
+    assert not ffv1.gpu_decodable({"fourcc": b"FFV1", "w": 640, "h": 360, "extradata": gen[:-1] + b"\0"})
     rec = ffv1.Ffv1Encoder("yuv422p10le", 640, 360, slices=(4, 4), host_only=True).extradata
     base = {"fourcc": b"FFV1", "w": 640, "h": 360}
     assert ffv1.is_pixpath_ffv1(dict(base, extradata=rec))
@@ -241,7 +247,7 @@ def test_codec_provenance_in_the_p03_log_line(monkeypatch):
     the codec and slice grid; with PIXPATH_FFV1=ffmpeg it carries the
     reference's own FFV1 options (the reference-faithful bitstream)."""
     from pixpath import ffmpeg as pff
-    from pixpath.provenance import p03_log_line
+    from p03_log import p03_log_line
     args = ["-y", "--input", "/db/videoSegments/seg.mkv", "--size", "1920x1080", "--pix-fmt", "yuv422p10le",
             "--vopts", pff.FFV1_OPTS, "--aopts", "-c:a flac", "/db/avpvs/P.avi"]
     monkeypatch.delenv("PIXPATH_FFV1", raising=False)

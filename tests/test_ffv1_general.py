@@ -1,0 +1,167 @@
+"""General FFV1 version 3 streams -- what the reference's AVPVS encode
+`ffmpeg -c:v ffv1 -threads 4 -level 3 -coder 1 -context 1 -slicecrc 1`
+(/root/reference/lib/ffmpeg.py:993, :1047) writes and pixpath's own encoder
+does not: a transmitted state table, 5-input context sets (several of them,
+chosen per slice), initial context states, and GOPs whose context states carry
+from frame to frame.
+
+CPU side (this file): the oracle's general restatement (oracle/ffv1_oracle.c,
+"General FFV1 version 3") round-trips every feature, reproduces pixpath's
+intra packets byte for byte when given pixpath's profile, and the product's
+record parser (pp_ffv1_decoder_create, host only) reads what it writes.  The
+GPU decode of these streams is tests/test_gpu_ffv1_general.py.  FFmpeg itself
+is absent, so parity against FFmpeg's own files stays unpinned."""
+import numpy as np
+import pytest
+
+import ffv1_ref as ref
+import pyoracle as po
+import synth
+
+FMTS = [("yuv422p10le", po.YUV422P10LE, 10, 1, 0), ("yuv420p", po.YUV420P, 8, 1, 1),
+        ("yuv420p10le", po.YUV420P10LE, 10, 1, 1), ("yuv422p", po.YUV422P, 8, 1, 0)]
+
+
+def _frames(rng, fid, w, h, n):
+    return [synth.noise_frame(rng, fid, w, h) if i % 3 == 1 else synth.smooth_frame(i, fid, w, h) for i in range(n)]
+
+
+def _init_states(sets, k, seed):
+    """Transmitted initial states for set k: what a 2-pass FFmpeg encode
+    stores (trained probabilities), here seeded values in 1..255."""
+    rng = np.random.default_rng(seed)
+    return rng.integers(1, 256, (ref.context_count(sets[k]), 32), dtype=np.uint8)
+
+
+def ffmpeg_like(bits, hs, vs, nh=2, nv=2, gop=12, init=False, tidx=(1, 1), sets=None):
+    sets = sets or ref.ffmpeg_context1_sets(bits)
+    ini = {i: _init_states(sets, i, 7 + i) for i in set(tidx)} if init else None
+    return ref.make_prof(bits, hs, vs, nh, nv, sets, tidx=tidx, coder=2, init=ini, gop=gop)
+
+
+@pytest.mark.parametrize("name,fid,bits,hs,vs", FMTS, ids=[f[0] for f in FMTS])
+@pytest.mark.parametrize("grid", [(3, 2), (1, 1), (4, 4)])
+def test_pixpath_profile_equals_the_intra_restatement(name, fid, bits, hs, vs, grid):
+    """The general encoder given pixpath's profile (default table, one 3-input
+    set, intra) writes the packets of the intra restatement the GPU encoder is
+    tested against: the sample-buffer border rules of the general path agree
+    with the intra path's neighbour rules."""
+    rng = np.random.default_rng(bits * 7 + grid[0])
+    w, h = 330, 190
+    pf = ref.make_prof(bits, hs, vs, *grid, [[ref.PIXPATH3] * 3 + [ref.ZERO] * 2], tidx=(0, 0), coder=1, gop=1)
+    enc = ref.GenEncoder(pf, w, h)
+    for f in (synth.noise_frame(rng, fid, w, h), synth.smooth_frame(2, fid, w, h)):
+        assert enc.encode(f) == ref.encode_frame(f, bits, hs, vs, *grid)
+
+
+@pytest.mark.parametrize("name,fid,bits,hs,vs", FMTS, ids=[f[0] for f in FMTS])
+@pytest.mark.parametrize("init", [False, True], ids=["states128", "initial_states"])
+def test_ffmpeg_like_sequence_round_trips(name, fid, bits, hs, vs, init):
+    """Custom state table, -context 1's two sets (5-input slices), GOP 3 with
+    states carried: every frame decodes back; keyframes where the GOP says."""
+    rng = np.random.default_rng(bits + 3 * hs + vs + init)
+    w, h = 200, 120
+    pf = ffmpeg_like(bits, hs, vs, gop=3, init=init)
+    x = ref.gen_extradata(pf)
+    dec = ref.GenDecoder(x, w, h)
+    assert dec.info["coder_type"] == 2 and dec.info["quant_table_sets"] == 2 and dec.info["intra"] == 0
+    assert dec.info["context_count1"] == (7563 if bits == 8 else 5063)
+    assert dec.info["initial_states1"] == int(init)
+    enc = ref.GenEncoder(pf, w, h)
+    for i, f in enumerate(_frames(rng, fid, w, h, 7)):
+        rc, out, key = dec.decode(enc.encode(f))
+        assert rc == 0 and key == (i % 3 == 0)
+        for p in range(3):
+            np.testing.assert_array_equal(out[p], f[p], err_msg="frame %d plane %d" % (i, p))
+
+
+def test_table_sets_per_plane_and_three_sets():
+    """Three sets, luma on set 2 (5-input), chroma on set 0 (3-input), with
+    initial states on both: the slice header's per-plane set index."""
+    rng = np.random.default_rng(5)
+    w, h, bits = 160, 96, 10
+    a, b = ref.QUANT9_10, ref.QUANT5_10
+    sets = [[a, a, a, ref.ZERO, ref.ZERO], [a, a, b, b, b], [b, a, b, ref.QUANT5, b]]
+    pf = ffmpeg_like(bits, 1, 0, 3, 1, gop=4, init=True, tidx=(2, 0), sets=sets)
+    x = ref.gen_extradata(pf)
+    dec = ref.GenDecoder(x, w, h)
+    enc = ref.GenEncoder(pf, w, h)
+    for i, f in enumerate(_frames(rng, po.YUV422P10LE, w, h, 6)):
+        rc, out, key = dec.decode(enc.encode(f))
+        assert rc == 0
+        for p in range(3):
+            np.testing.assert_array_equal(out[p], f[p])
+
+
+def test_states_carry_across_frames():
+    """An inter frame's packet depends on the frames before it in its GOP:
+    the same picture coded as the second frame of a GOP differs from its
+    keyframe coding, and decoding it without its GOP's first frame fails."""
+    rng = np.random.default_rng(8)
+    w, h = 128, 64
+    f0, f1 = synth.noise_frame(rng, po.YUV420P, w, h), synth.noise_frame(rng, po.YUV420P, w, h)
+    pf = ffmpeg_like(8, 1, 1, gop=2)
+    enc = ref.GenEncoder(pf, w, h)
+    p0, p1 = enc.encode(f0), enc.encode(f1)
+    assert p1 != ref.GenEncoder(pf, w, h).encode(f1)
+    dec = ref.GenDecoder(ref.gen_extradata(pf), w, h)
+    assert dec.decode(p1)[0] == -6  # non-keyframe first
+    assert dec.decode(p0)[0] == 0
+    rc, out, key = dec.decode(p1)
+    assert rc == 0 and key == 0 and all(np.array_equal(out[p], f1[p]) for p in range(3))
+
+
+def test_record_crc_and_state_table_checks():
+    pf = ffmpeg_like(10, 1, 0)
+    x = bytearray(ref.gen_extradata(pf))
+    x[5] ^= 1
+    with pytest.raises(ValueError):
+        ref.GenDecoder(bytes(x), 64, 64)
+
+
+# ---- the product's record parser (host only) ---------------------------------
+
+def _native_info(dec):
+    import ctypes
+    from pixpath._native import check, lib
+    info = (ctypes.c_int * 8)()
+    n = check(lib().pp_ffv1_decoder_info(dec.handle, info, 8))
+    return dict(zip(("micro", "coder", "tables", "max_ctx", "intra", "ec", "init_mask", "pix"), list(info)[:n]))
+
+
+@pytest.mark.parametrize("name,fid,bits,hs,vs", FMTS, ids=[f[0] for f in FMTS])
+@pytest.mark.parametrize("init", [False, True], ids=["states128", "initial_states"])
+def test_product_parser_reads_ffmpeg_like_records(name, fid, bits, hs, vs, init):
+    """pp_ffv1_decoder_create accepts the general records (the round-4
+    parser refused coder 2, two sets, 5-input tables and inter frames) and
+    reads the same fields the restatement's decoder reads."""
+    from pixpath import ffv1
+    pf = ffmpeg_like(bits, hs, vs, init=init)
+    x = ref.gen_extradata(pf)
+    dec = ffv1.Ffv1Decoder(x, 1920, 1080, host_only=True)
+    assert dec.fmt.name == name and dec.slices == (2, 2)
+    info = _native_info(dec)
+    assert info == {"micro": 4, "coder": 2, "tables": 2, "max_ctx": 7563 if bits == 8 else 5063, "intra": 0,
+                    "ec": 1, "init_mask": 2 if init else 0, "pix": 0}
+    # 2 line rows per slice for the 5-input context: 960-sample rows, 16 per workgroup
+    assert (dec.slices_per_workgroup, dec.row_cap) == (16, 960)
+
+
+@pytest.mark.parametrize("name,fid,bits,hs,vs", FMTS, ids=[f[0] for f in FMTS])
+def test_product_parser_marks_pixpath_records(name, fid, bits, hs, vs):
+    from pixpath import ffv1
+    dec = ffv1.Ffv1Decoder(ref.extradata(bits, hs, vs, 8, 8), 1920, 1080, host_only=True)
+    assert _native_info(dec) == {"micro": 4, "coder": 1, "tables": 1, "max_ctx": 666, "intra": 1, "ec": 1,
+                                 "init_mask": 0, "pix": 1}
+
+
+def test_product_parser_refuses_corrupt_records():
+    from pixpath import ffv1
+    x = ref.gen_extradata(ffmpeg_like(8, 1, 1, init=True))
+    for k in (3, len(x) // 2, len(x) - 6):
+        bad = bytearray(x)
+        bad[k] ^= 0x10
+        with pytest.raises(Exception, match="CRC"):
+            ffv1.Ffv1Decoder(bytes(bad), 640, 360, host_only=True)
+    with pytest.raises(Exception):
+        ffv1.Ffv1Decoder(x[:12], 640, 360, host_only=True)

@@ -76,3 +76,18 @@ def test_product_decoder_reads_the_record(name, fid, bits, hs, vs):
     bad[3] ^= 0x04
     with pytest.raises(Exception, match="CRC"):
         ffv1.Ffv1Decoder(bytes(bad), 1920, 1080, host_only=True)
+
+
+@pytest.mark.parametrize("w,grid,lpw,cap", [(1920, (8, 8), 16, 240), (1920, (1, 1), 16, 1920), (3840, (2, 2), 16, 1920),
+                                            (4912, (1, 1), 16, 4912), (4992, (1, 1), 15, 4992), (5120, (1, 1), 15, 5120),
+                                            (16384, (1, 1), 4, 16384), (1000, (3, 1), 16, 336)])
+def test_decoder_geometry_fits_the_lds(w, grid, lpw, cap):
+    """The decoder's slices per workgroup (pp_ffv1_decoder_geometry, host
+    only): the widest slice row rounded to 8 samples, 2 B per sample per slice
+    within the 156 KB of dynamic LDS less the record's quantisation tables
+    (2.5 KB per set); 16 slices up to 4,912-sample rows, fewer beyond (the path
+    tests/test_gpu_ffv1.py's wide-row cases run)."""
+    x = ref.extradata(10, 1, 0, *grid)
+    dec = ffv1.Ffv1Decoder(x, w, 64, host_only=True)
+    assert (dec.slices_per_workgroup, dec.row_cap) == (lpw, cap)
+    assert 2560 + lpw * cap * 2 <= 160 * 1024 - 4096

@@ -417,3 +417,35 @@ def test_failed_writer_leaves_no_file_and_frees_its_encoder(gpu, tmp_path, monke
     again = ffv1.acquire_encoder("yuv422p10le", 320, 180, slices=(4, 4), max_frames=8, device=gpu)
     assert again is not enc
     torch.cuda.synchronize()
+
+
+WIDE = [(1920, 64, (1, 1), 3, 16), (5120, 16, (1, 1), 20, 15), (16384, 8, (1, 1), 6, 4),
+        (1920, 1080, (1, 1), 1, 16), (1920, 1080, (2, 1), 2, 16), (1920, 1080, (2, 2), 2, 16),
+        (3840, 2160, (2, 2), 1, 16)]
+
+
+@pytest.mark.parametrize("name,fid,bits,hs,vs", [CASES[0], CASES[1]], ids=[CASES[0][0], CASES[1][0]])
+@pytest.mark.parametrize("w,h,grid,n,lpw", WIDE, ids=["%dx%d-%dx%d" % (c[0], c[1], *c[2]) for c in WIDE])
+def test_gpu_decoder_wide_slice_rows(gpu, name, fid, bits, hs, vs, w, h, grid, n, lpw):
+    """Slice rows wider than 1,216 samples: the decoder sizes its
+    slices per workgroup to the LDS line buffers -- 16 up to 4,912-sample rows,
+    fewer beyond (5120 -> 15, 16384 -> 4, with frames spread over several
+    workgroups, the last one partial).  GPU encode -> GPU decode returns the
+    input; the C restatement's packets equal the GPU's and decode on the GPU."""
+    from pixpath import ffv1
+    rng = np.random.default_rng(w + h + n)
+    frames = [synth.smooth_frame(i, fid, w, h) if i % 2 else synth.noise_frame(rng, fid, w, h) for i in range(n)]
+    enc = ffv1.Ffv1Encoder(name, w, h, slices=grid, max_frames=n, device=gpu)
+    pkts = enc.encode_to_host(_batch(gpu, name, frames))
+    dec = ffv1.Ffv1Decoder(enc.extradata, w, h, max_frames=n, device=gpu)
+    assert (dec.slices_per_workgroup, dec.row_cap) == (lpw, -(-(w // grid[0]) // 8) * 8)
+    out = dec.decode(b"".join(pkts), [len(p) for p in pkts]).to_numpy()
+    for f, planes in enumerate(frames):
+        for p in range(3):
+            np.testing.assert_array_equal(out[p][f], planes[p], err_msg="frame %d plane %d" % (f, p))
+    for f in sorted({0, n - 1}):
+        want = ref.encode_frame(frames[f], bits, hs, vs, *grid)
+        assert pkts[f] == want, "frame %d: GPU packet differs from the C restatement's" % f
+        out1 = dec.decode(want, [len(want)]).to_numpy()
+        for p in range(3):
+            np.testing.assert_array_equal(out1[p][0], frames[f][p])
