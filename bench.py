@@ -508,12 +508,13 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None, shared=True):
         order = sorted(stats, key=lambda w: w["timeline"][0][0] if w["timeline"] else 0)
         st = {"setup_s": setup_s, "pipeline_s": pipe_s, "tail_s": round(t_end - t_main, 4),
               # per PVS, seconds from the run's start: batch queued, frames ready on the
-              # GPU (encode starts), packets on the host, packets written, AVI closed
+              # GPU (encode starts), encode done (packet D2H starts), packets written
+              # (D2H chunks overlapped with the writes), AVI closed
               "timeline": [[round(x - t0, 4) for x in (w["timeline"][0][0], w["timeline"][0][2],
                                                        w["timeline"][0][3], w["timeline"][0][4], w["closed_at"])]
                            for w in order if w["timeline"]],
-              "encode_and_d2h_s": [round(w["encode_s"], 4) for w in order],
-              "avi_write_s": [round(w["write_s"], 4) for w in order],
+              "encode_s": [round(w["encode_s"], 4) for w in order],
+              "d2h_and_avi_write_s": [round(w["write_s"], 4) for w in order],
               "encode_launches": [w["launches"] for w in order]}
         # the main thread's stages plus the wait for the last writers: the wall time
         st["explained_s"] = round(sum(setup_s) + sum(pipe_s) + st["tail_s"], 4)

@@ -18,7 +18,12 @@
 //   * the swscale filter construction (filters.cpp FilterBank::build /
 //     compact) for random sizes, flags and parameters.
 //
-// usage: fuzz_host [iterations (default 20000)] [seed]
+//   * general FFV1 records given as seeds (file of u32-LE-length-prefixed
+//     records: the oracle's FFmpeg-like records with transmitted state
+//     tables, 5-input table sets and initial states) -- each must parse, then
+//     its mutations must never read outside the buffer.
+//
+// usage: fuzz_host [iterations (default 20000)] [seed] [seed-record file]
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -108,6 +113,39 @@ long fuzz_records(Rng &r, int iters) {
         for (int k = 1 + r.below(3); k; --k) mutate(r, m);
         std::vector<uint8_t> b = exact(m);
         (void)ffv1_parse_record(b.empty() ? nullptr : b.data(), (int)b.size(), w, h, &out, &err);
+        ++n;
+    }
+    return n;
+}
+
+long fuzz_seed_records(Rng &r, int iters, const char *path) {
+    std::vector<std::vector<uint8_t>> seeds;
+    if (FILE *f = std::fopen(path, "rb")) {
+        uint8_t hdr[4];
+        while (std::fread(hdr, 1, 4, f) == 4) {
+            const uint32_t n = hdr[0] | hdr[1] << 8 | hdr[2] << 16 | (uint32_t)hdr[3] << 24;
+            std::vector<uint8_t> b(n);
+            if (std::fread(b.data(), 1, n, f) != n) break;
+            seeds.push_back(std::move(b));
+        }
+        std::fclose(f);
+    }
+    CHECK(!seeds.empty(), "no seed records in %s", path);
+    long n = 0;
+    for (size_t k = 0; k < seeds.size(); ++k) {
+        pp::Ffv1Record out;
+        std::string err;
+        std::vector<uint8_t> b = exact(seeds[k]);
+        const int rc = ffv1_parse_record(b.data(), (int)b.size(), 1920, 1080, &out, &err);
+        CHECK(rc == 0, "seed record %zu refused: %s", k, err.c_str());
+    }
+    for (int it = 0; it < iters && !seeds.empty(); ++it) {
+        std::vector<uint8_t> m = seeds[r.below((int)seeds.size())];
+        for (int k = 1 + r.below(3); k; --k) mutate(r, m);
+        std::vector<uint8_t> b = exact(m);
+        pp::Ffv1Record out;
+        std::string err;
+        (void)ffv1_parse_record(b.empty() ? nullptr : b.data(), (int)b.size(), 1920, 1080, &out, &err);
         ++n;
     }
     return n;
@@ -247,6 +285,7 @@ int main(int argc, char **argv) {
     const long b = fuzz_packets(r, iters);
     const long c = fuzz_scanners(r, iters / 4);
     const long d = fuzz_filters(r, iters / 20);
-    std::printf("records %ld packets %ld scans %ld filters %ld failures %d\n", a, b, c, d, g_fail);
+    const long e = argc > 3 ? fuzz_seed_records(r, iters, argv[3]) : 0;
+    std::printf("records %ld packets %ld scans %ld filters %ld seeded %ld failures %d\n", a, b, c, d, e, g_fail);
     return g_fail ? 1 : 0;
 }

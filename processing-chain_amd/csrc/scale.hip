@@ -443,6 +443,10 @@ struct pp_scale_plan {
     // takes the 16-row chunks and ring2 LDS the chroma planes need
     pp_scale_plan *luma = nullptr;
     size_t fast_lds_plane[2] = {0, 0};  // strip_kernel LDS of the luma / chroma jobs alone
+    size_t fast_lds_direct = 0;         // strip_kernel DIRECT instances (8-bit source, HW 8): the V window ring only
+    std::vector<int32_t> chroma_lo, chroma_hi;  // chain first stage: source rows of each chroma chunk (host copy)
+    hipStream_t side = nullptr;       // CHAIN with `luma`: the luma launch's stream when the two launches overlap
+    hipEvent_t fork = nullptr, join = nullptr;
 };
 
 namespace {
@@ -773,6 +777,7 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
                 hp[c].S_fast = std::max(hp[c].f_S, (hp[c].max_base + 2 * HW + 15) & ~15);
                 P->fast_lds_plane[c] = (size_t)hp[c].maxnew * hp[c].S_fast * 2 + (size_t)hp[c].ring * ftw * 2;
                 lds = std::max(lds, P->fast_lds_plane[c]);
+                P->fast_lds_direct = std::max(P->fast_lds_direct, (size_t)hp[c].ring * ftw * 2);
             }
             if (HW > 0 && lds <= lds_budget() * (size_t)(ftw / 256)) {
                 P->fast_hw = HW;
@@ -815,6 +820,10 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
             fbase += F.tiles_x * F.tiles_y;
         }
         P->fast_tiles = fbase;
+    }
+    if (one_seg_chroma) {  // the chain plan re-sizes the chroma staging for its segments
+        P->chroma_lo = hp[1].lo;
+        P->chroma_hi = hp[1].hi;
     }
     if (!ctx) {
         *out = P.release();
@@ -950,7 +959,7 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
               (identity_bank(p2->f[0], 1 << 14) && identity_bank(p2->f[1], 1 << 14) &&
                identity_bank(p2->f[2], 1 << 12) && (v422 || identity_bank(p2->f[3], 1 << 12)));
     std::vector<int32_t> vrow2, chunk2, seg2;
-    int vtp2 = 0, ring2 = 0;
+    int vtp2 = 0, ring2 = 0, maxnew2 = 0;
     if (ok && v422) {
         // second-stage chroma rows: compact window, tap pairs, record per row
         const int cdh1 = P->cdh, dh2 = p2->cdh;
@@ -1005,7 +1014,16 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
             seg2[4 * sg + 1] = std::min(cdh1, (need[r1 - 1] / cho + 1) * cho);
             seg2[4 * sg + 2] = r0;
             seg2[4 * sg + 3] = r1;
+            // a segment's first chunk stages its whole source window, not only
+            // the rows new to a walk from the top: the staging buffer grows to it
+            const int c0 = seg2[4 * sg] / cho;
+            maxnew2 = std::max(maxnew2, P->chroma_hi[c0] - P->chroma_lo[c0]);
         }
+    }
+    if (maxnew2 > P->fjob[1].maxnew) {
+        for (int p = 1; p < 3; ++p) P->fjob[p].maxnew = maxnew2;
+        P->fast_lds_plane[1] = (size_t)maxnew2 * P->fjob[1].S * 2 + (size_t)P->fjob[1].ring * P->fast_tw * 2;
+        P->fast_lds = std::max(P->fast_lds, P->fast_lds_plane[1]);
     }
     // the byte ring is circular: a power of two of rows >= every chunk's live span
     int r2rows = 2;
@@ -1018,7 +1036,8 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
     // luma as its own launch (4:2:2 targets: the chroma launch then carries
     // only the ring2 planes): its plan is the plain first stage, same filters
     pp_scale_plan *lp = nullptr;
-    if (v422 && plan_create(ctx, src_fmt, sw, sh, PP_FMT_YUV420P, dw, dh, flags, p0, p1, false, &lp) == PP_OK) {
+    // PIXPATH_CHAIN_ONE_LAUNCH (measurement build): keep luma in the chroma launch
+    if (v422 && !PP_KNOB("PIXPATH_CHAIN_ONE_LAUNCH") && plan_create(ctx, src_fmt, sw, sh, PP_FMT_YUV420P, dw, dh, flags, p0, p1, false, &lp) == PP_OK) {
         if (lp->kind == pp_scale_plan::GENERIC && lp->fast_hw > 0 && lp->fast_tw == 256) {
             P->luma = lp;
             lp->fjob[0].fuse = P->chain_out > 8 ? 1 : 0;
@@ -1063,6 +1082,9 @@ extern "C" int pp_scale_plan_destroy(pp_scale_plan *P) {
     if (!P) return PP_OK;
     if (P->stage2) (void)pp_scale_plan_destroy(P->stage2);
     if (P->luma) (void)pp_scale_plan_destroy(P->luma);
+    if (P->side) (void)hipStreamDestroy(P->side);
+    if (P->fork) (void)hipEventDestroy(P->fork);
+    if (P->join) (void)hipEventDestroy(P->join);
     if (P->dev2) (void)hipFree(P->dev2);
     if (P->dev) (void)hipFree(P->dev);
     if (P->scratch) (void)hipFree(P->scratch);
@@ -1143,6 +1165,10 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
         const int vtm = strip_vtm_bucket(std::max(P->fjob[0].vtp, P->fjob[1].vtp));
         k = P->si.depth == 8 ? pick_strip_u8(out_depth, P->fast_hw, vtm, P->fast_tw)
                              : pick_strip_u16(out_depth, P->fast_hw, vtm, P->fast_tw);
+        if (P->si.depth == 8 && P->fast_hw == 8) {  // strip_kernel DIRECT: no staged rows in LDS
+            for (int p = 0; p < 3; ++p) a.pl[p].maxnew = 0;
+            lds = P->fast_lds_direct;
+        }
     } else if (P->si.depth == 8) {
         k = out_depth == 8 ? pick_ht<uint8_t, 8>(P->ht, tw256) : pick_ht<uint8_t, 10>(P->ht, tw256);
     } else {
@@ -1257,14 +1283,33 @@ int launch_chain_planes(pp_scale_plan *P, const pp::PlaneJob *const *jobs, const
 int launch_chain(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, int nframes, hipStream_t st) {
     using namespace pp;
     if (P->luma) {
+        // PIXPATH_CHAIN_OVERLAP (measurement build): the luma launch on a side
+        // stream, concurrent with the chroma launch (fork / join events on `st`)
+        const bool overlap = PP_KNOB("PIXPATH_CHAIN_OVERLAP") != nullptr;
+        hipStream_t ls = st;
+        if (overlap) {
+            if (!P->side) {
+                PP_HIP(hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking));
+                PP_HIP(hipEventCreateWithFlags(&P->fork, hipEventDisableTiming));
+                PP_HIP(hipEventCreateWithFlags(&P->join, hipEventDisableTiming));
+            }
+            PP_HIP(hipEventRecord(P->fork, st));
+            PP_HIP(hipStreamWaitEvent(P->side, P->fork, 0));
+            ls = P->side;
+        }
         const PlaneJob *lj[1] = {&P->luma->fjob[0]};
         const int lpl[1] = {0};
         if (int rc = launch_chain_planes(P, lj, lpl, 1, P->luma->fast_hw, P->luma->fast_lds_plane[0], src, dst,
-                                         nframes, st))
+                                         nframes, ls))
             return rc;
         const PlaneJob *cj[2] = {&P->fjob[1], &P->fjob[2]};
         const int cpl[2] = {1, 2};
-        return launch_chain_planes(P, cj, cpl, 2, P->fast_hw, P->chain_lds, src, dst, nframes, st);
+        const int rc = launch_chain_planes(P, cj, cpl, 2, P->fast_hw, P->chain_lds, src, dst, nframes, st);
+        if (overlap) {
+            PP_HIP(hipEventRecord(P->join, P->side));
+            PP_HIP(hipStreamWaitEvent(st, P->join, 0));
+        }
+        return rc;
     }
     const PlaneJob *jobs[3] = {&P->fjob[0], &P->fjob[1], &P->fjob[2]};
     const int pl[3] = {0, 1, 2};

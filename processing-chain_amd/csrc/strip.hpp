@@ -139,6 +139,12 @@ constexpr bool strip_clamp_path() {
 template <typename ST, int OUTB, int HW, int VTM, int FUSE = 0, int TW = 256>
 __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() : strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
     static_assert(TW == 256 || TW == 512, "strip width");
+    // DIRECT (8-bit sources, 8-dword windows: the 2:1 downscales of config 3):
+    // no staged source rows -- a lane loads its window's 16 source bytes of a
+    // row straight into registers for the H pass, so the plan's LDS is the V
+    // window ring alone (the staged rows, widened to 16 bits, were two thirds
+    // of it and kept the chunks at 8 rows)
+    constexpr bool DIRECT = sizeof(ST) == 1 && HW == 8 && FUSE == 0;
     extern __shared__ __align__(16) uint16_t lds[];
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int frame = L / a.tiles;
@@ -194,6 +200,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
     }
 
     // ---- staging (16-B loads through the plane's buffer resource) ----------
+    // (DIRECT: the plan passes maxnew = 0, so `win` starts the LDS)
     constexpr int CH = 16 / sizeof(ST);
     const int cpr = (cn + CH - 1) / CH;  // 16-B chunks per staged row (<= TW, host-checked)
     const int64_t sls = a.sls[p];
@@ -267,8 +274,10 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
     // Between those two points the wave issues no vector-memory op, so the
     // wait for the loads never covers this wave's V-pass stores (vmcnt is
     // in-order over loads and stores).
-    prefetch(pf, next_src, chunk_hi[y_begin / cho]);
-    commit(pf, next_src, chunk_hi[y_begin / cho]);
+    if constexpr (!DIRECT) {
+        prefetch(pf, next_src, chunk_hi[y_begin / cho]);
+        commit(pf, next_src, chunk_hi[y_begin / cho]);
+    }
     const bool lane_any = cx < nx, lane_full = cx + 4 <= nx;
     const int xo = x0 + cx;
     // clamped V pass (wave-uniform): when the strip ends on a 4-column group
@@ -298,7 +307,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
         const int after = nnew > 0 ? hi : next_src;
         const bool more = y0 + cho < y_end;
         const int nfrom = more ? max(after, chunk_lo[ci + 1]) : 0, nhi = more ? chunk_hi[ci + 1] : 0;
-        if (more && !(PP_ABLATE(a.debug) & 2)) prefetch(pf, nfrom, nhi);
+        if (!DIRECT && more && !(PP_ABLATE(a.debug) & 2)) prefetch(pf, nfrom, nhi);
         // kept row pairs move down to the window start, each column by its own
         // lane in increasing order (no lane reads a slot already overwritten)
         bool moved = false;
@@ -310,7 +319,66 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
         base = nbase;
         // ---- horizontal pass: row pairs of the window, wave-strided ----------
         if (nnew > 0 && (PP_ABLATE(a.debug) & 4)) next_src = hi;
-        if (nnew > 0 && !(PP_ABLATE(a.debug) & 4)) {
+        if (DIRECT && nnew > 0 && !(PP_ABLATE(a.debug) & 4)) {
+            // window row i = source row base + i; a lane's 16 bytes at its
+            // window base (dword aligned: c0 % 16 == 0, hb % 4 == 0)
+            const int i0 = next_src - base;
+            const int kf0 = (i0 + 1) >> 1, kf1 = (i0 + nnew) >> 1;
+            const int hoff = cbyte + hb;
+            auto ld = [&](int i) { return bload16(rs, (base + i) * (int)sls + hoff); };
+            auto hregs = [&](const uint4 r, int out[4]) {  // hrow4 on register-held bytes
+                const uint32_t d4[4] = {r.x, r.y, r.z, r.w};
+                uint32_t w[HW];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    w[2 * m] = __builtin_amdgcn_perm(0u, d4[m], 0x0c010c00u);
+                    w[2 * m + 1] = __builtin_amdgcn_perm(0u, d4[m], 0x0c030c02u);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    int acc = dot2_first(__builtin_bit_cast(v2i16, w[0]), hc[j][0]);
+#pragma unroll
+                    for (int d = 1; d < HW; ++d)
+                        acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, w[d]), hc[j][d], acc, false);
+                    acc >>= hshift;
+                    out[j] = acc < 32767 ? acc : 32767;
+                }
+            };
+            auto pair_out = [&](int k, const uint4 ra, const uint4 rb) {
+                int oa[4], ob[4];
+                hregs(ra, oa);
+                hregs(rb, ob);
+                uint4 v;
+                v.x = __builtin_amdgcn_perm(ob[0], oa[0], 0x05040100u);
+                v.y = __builtin_amdgcn_perm(ob[1], oa[1], 0x05040100u);
+                v.z = __builtin_amdgcn_perm(ob[2], oa[2], 0x05040100u);
+                v.w = __builtin_amdgcn_perm(ob[3], oa[3], 0x05040100u);
+                *reinterpret_cast<uint4 *>(win + k * TW + cx) = v;
+            };
+            if ((i0 & 1) && rg == ((i0 >> 1) & 3)) {  // high row of a kept pair
+                int o[4];
+                hregs(ld(i0), o);
+                uint16_t *w16 = reinterpret_cast<uint16_t *>(win + (i0 >> 1) * TW + cx);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) w16[2 * j + 1] = static_cast<uint16_t>(o[j]);
+            }
+            if (((i0 + nnew) & 1) && rg == (kf1 & 3)) {  // low row of the last pair
+                int o[4];
+                hregs(ld(i0 + nnew - 1), o);
+                uint4 v;
+                v.x = o[0] & 0xffff; v.y = o[1] & 0xffff; v.z = o[2] & 0xffff; v.w = o[3] & 0xffff;
+                *reinterpret_cast<uint4 *>(win + kf1 * TW + cx) = v;
+            }
+            int k = kf0 + rg;
+            for (; k + 4 < kf1; k += 8) {  // two pairs a step: four row loads in flight
+                const uint4 a0 = ld(2 * k), a1 = ld(2 * k + 1), b0 = ld(2 * k + 8), b1 = ld(2 * k + 9);
+                pair_out(k, a0, a1);
+                pair_out(k + 4, b0, b1);
+            }
+            if (k < kf1) pair_out(k, ld(2 * k), ld(2 * k + 1));
+            next_src = hi;
+        }
+        if (!DIRECT && nnew > 0 && !(PP_ABLATE(a.debug) & 4)) {
             const int i0 = next_src - base;
             const int kf0 = (i0 + 1) >> 1, kf1 = (i0 + nnew) >> 1;
             if ((i0 & 1) && rg == ((i0 >> 1) & 3)) {  // high row of a kept pair
@@ -342,7 +410,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
             next_src = hi;
         }
         if (!(PP_ABLATE(a.debug) & 8)) __syncthreads();  // window complete; src_t is free
-        if (more && nhi > nfrom && !(PP_ABLATE(a.debug) & 2)) commit(pf, nfrom, nhi);
+        if (!DIRECT && more && nhi > nfrom && !(PP_ABLATE(a.debug) & 2)) commit(pf, nfrom, nhi);
         // ---- vertical pass: one output row per wave --------------------------
         // raised priority while the wave issues its output rows: the other
         // waves' H pass never starves the write stream (-2 %, profiles/r2)

@@ -112,6 +112,34 @@ class Ffv1Encoder:
             check(lib().pp_stream_synchronize(st))
         return self._host[:n].numpy()
 
+    def packets_to_host_chunks(self, ptr, n, sizes, stream, chunk=128 << 20):
+        """The last encode's packets D2H in packet-aligned chunks of about
+        `chunk` bytes, all queued at once on `stream`; yields (numpy view,
+        frame sizes) of each chunk as its copy lands, so the caller writes
+        chunk k while chunk k + 1 is still in flight (the views stay valid
+        until the next call)."""
+        if getattr(self, "_host", None) is None or self._host.numel() < n:
+            self._host = torch.empty(max(n + n // 4, 1 << 20), dtype=torch.uint8).pin_memory()
+        st = ctypes.c_void_p(stream.cuda_stream)
+        parts, i0, b0, acc = [], 0, 0, 0
+        for i, k in enumerate(sizes.tolist()):
+            acc += k
+            if acc - b0 >= chunk or i == len(sizes) - 1:
+                parts.append((i0, i + 1, b0, acc))
+                i0, b0 = i + 1, acc
+        evs = []
+        for _, _, lo, hi in parts:
+            if hi > lo:
+                check(lib().pp_copy_async(ctypes.c_void_p(self._host.data_ptr() + lo), ctypes.c_void_p(ptr + lo),
+                                          hi - lo, PP_COPY_D2H, st))
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            evs.append(ev)
+        host = self._host.numpy()
+        for (a, b, lo, hi), ev in zip(parts, evs):
+            ev.synchronize()
+            yield host[lo:hi], sizes[a:b]
+
     def encode_host(self, src, stream=None):
         """(numpy uint8 view of the packets in a pinned host buffer, frame sizes):
         encode, then one D2H of the packets straight from the encoder's packet
@@ -394,9 +422,11 @@ class Ffv1AviWriter:
                     # upload (put_stream, synchronised per upload) waits behind it
                     # (ADVICE r4); the D2H waits for the encode on its stream
                     self.d2h_stream.wait_stream(self.stream)
-                    data = self.enc.packets_to_host(ptr, n, self.d2h_stream)
                     t1 = time.perf_counter()
-                    self.avi.write_packets(data, sizes)
+                    # packets D2H in chunks, each written to the AVI as it lands
+                    # (the copy of chunk k + 1 overlaps the write of chunk k)
+                    for data, part in self.enc.packets_to_host_chunks(ptr, n, sizes, self.d2h_stream):
+                        self.avi.write_packets(data, part)
                     t2 = time.perf_counter()
                     self.stats["encode_s"] += t1 - t0
                     self.stats["write_s"] += t2 - t1

@@ -15,11 +15,11 @@ for step in "$@"; do
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?
       echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu_$TAG.log; grep -E "^(FAILED|ERROR)" gpurun_out/pytest_gpu_$TAG.log | head -20
-      [ $rc -gt 1 ] && { echo "stopping after pytest rc=$rc"; exit $rc; } ;;
+      if [ $rc -gt 1 ]; then echo "stopping after pytest rc=$rc"; exit $rc; fi ;;
     tests:*)
       timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "${step#tests:}" > gpurun_out/pytest_sel_$TAG.log 2>&1; rc=$?
       echo "pytest(${step#tests:}) rc=$rc"; tail -2 gpurun_out/pytest_sel_$TAG.log; grep -E "^(FAILED|ERROR)|Error" gpurun_out/pytest_sel_$TAG.log | head -20
-      [ $rc -gt 1 ] && { echo "stopping after pytest rc=$rc"; exit $rc; } ;;
+      if [ $rc -gt 1 ]; then echo "stopping after pytest rc=$rc"; exit $rc; fi ;;
     smoke)
       timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { tail -5 gpurun_out/smoke_$TAG.log; exit 1; }
       tail -1 gpurun_out/smoke_$TAG.log ;;

@@ -5,7 +5,10 @@ bench's warm-up steps, which include first-touch of fresh output batches) are
 dropped, so the mean is comparable with bench.py's HIP-event avg_launch_ms.
 
   python3 tools/trace_stats.py <run_kernel_trace.csv> <skip> [substring ...] > stats.csv
+  PIXPATH_TRACE_BY_GRID=1: launches of one kernel with different grid sizes
+  apart (e.g. the chain plan's luma and chroma launches of one instance)
 """
+import os
 import csv
 import statistics
 import sys
@@ -20,6 +23,9 @@ def main():
         name = r["Kernel_Name"]
         if want and not any(w in name for w in want):
             continue
+        if os.environ.get("PIXPATH_TRACE_BY_GRID"):
+            g = [r[k] for k in sorted(r) if k.startswith("Grid_Size")]
+            name = name.split("(")[0] + " grid=" + "x".join(g)
         d[name].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
     print("kernel,launches_total,launches_timed,mean_ms,median_ms,min_ms,max_ms,stdev_ms,warmup_mean_ms")
     for name, ev in sorted(d.items(), key=lambda kv: -sum(e - s for s, e in kv[1])):
