@@ -966,18 +966,48 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
         HostPlane h2;
         std::string err;
         if (p2->f[3].compact(cdh1, 1, &h2.v, &err)) PP_FAIL(PP_ERR_UNSUPPORTED, "%s", err.c_str());
-        pair_rows(h2);
-        vtp2 = h2.vtp;
-        ok = vtp2 <= 4;
         std::vector<int> need(dh2, 0);
-        vrow2.assign((size_t)dh2 * 16, 0);
         for (int r = 0; r < dh2; ++r) {
             int last = 0;
             for (int k = 0; k < h2.v.taps; ++k)
                 if (h2.v.coef[(size_t)r * h2.v.taps + k]) last = k;
             need[r] = h2.v.pos[r] + last;
-            vrow2[(size_t)r * 16] = h2.vbase[r];
-            for (int j = 0; j < vtp2 && j < 15; ++j) vrow2[(size_t)r * 16 + 1 + j] = h2.vcoef2[(size_t)r * vtp2 + j];
+        }
+        // rows in pairs (2m, 2m + 1) over one shared window (strip.hpp pass2):
+        // base = the even row at or below the pair's first non-zero tap, each
+        // row's non-zero taps placed at their rows within the window
+        const int npair = (dh2 + 1) / 2, T2 = h2.v.taps;
+        auto tap_rows = [&](int r, int *lo, int *hi) {
+            *lo = INT32_MAX;
+            *hi = -1;
+            for (int k = 0; k < T2; ++k)
+                if (h2.v.coef[(size_t)r * T2 + k]) {
+                    *lo = std::min(*lo, h2.v.pos[r] + k);
+                    *hi = std::max(*hi, h2.v.pos[r] + k);
+                }
+            if (*hi < 0) *lo = *hi = h2.v.pos[r];  // an all-zero row (none in practice)
+        };
+        std::vector<int> pbase(npair);
+        vtp2 = 1;
+        for (int m = 0; m < npair; ++m) {
+            int la, ha, lb, hb;
+            tap_rows(2 * m, &la, &ha);
+            tap_rows(std::min(2 * m + 1, dh2 - 1), &lb, &hb);
+            pbase[m] = std::min(la, lb) & ~1;
+            vtp2 = std::max(vtp2, (std::max(ha, hb) - pbase[m]) / 2 + 1);
+        }
+        ok = vtp2 <= 3;  // strip.hpp pass2 instances (registers: spill-free at 6 waves)
+        vrow2.assign((size_t)npair * 16, 0);
+        for (int m = 0; ok && m < npair; ++m) {
+            vrow2[(size_t)m * 16] = pbase[m];
+            uint16_t *t16 = reinterpret_cast<uint16_t *>(&vrow2[(size_t)m * 16 + 1]);
+            for (int h = 0; h < 2 && 2 * m + h < dh2; ++h)
+                for (int k = 0; k < T2; ++k) {
+                    const int16_t c = h2.v.coef[(size_t)(2 * m + h) * T2 + k];
+                    if (!c) continue;
+                    const int y = h2.v.pos[2 * m + h] + k - pbase[m];  // in [0, 2 * vtp2)
+                    t16[2 * (h * vtp2 + y / 2) + (y & 1)] = (uint16_t)c;
+                }
         }
         // per first-stage chunk: the second-stage rows it completes and the ring2 rows kept
         const int cho = P->fjob[1].cho, nch = (cdh1 + cho - 1) / cho;
@@ -986,15 +1016,17 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
         for (int ci = 0; ci < nch; ++ci) {
             const int y0 = ci * cho, end = std::min(cdh1, y0 + cho);
             const int lo2 = done;
-            while (done < dh2 && need[done] < end) ++done;
+            // pairs complete together (a pair's rows are computed at once)
+            while (done < dh2 && need[done] < end && (done + 1 >= dh2 || need[done + 1] < end))
+                done = std::min(dh2, done + 2);
             if (ci == nch - 1) done = dh2;
-            const int b2 = (std::min(lo2 < dh2 ? h2.vbase[lo2] : y0, y0)) & ~1;
+            const int b2 = (std::min(lo2 < dh2 ? pbase[lo2 / 2] : y0, y0)) & ~1;
             chunk2[4 * ci] = lo2;
             chunk2[4 * ci + 1] = done;
             chunk2[4 * ci + 2] = b2;
             chunk2[4 * ci + 3] = (y0 - b2 + 1) >> 1;
             int top = end;
-            for (int r = lo2; r < done; ++r) top = std::max(top, h2.vbase[r] + 2 * vtp2);
+            for (int m = lo2 / 2; m < (done + 1) / 2; ++m) top = std::max(top, pbase[m] + 2 * vtp2);
             ring2 = std::max(ring2, top - b2);
         }
         ring2 = (ring2 + 1) & ~1;
@@ -1009,8 +1041,10 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
         nseg2 = std::min(nseg2, std::max(1, dh2 / 16));
         seg2.assign((size_t)nseg2 * 4, 0);
         for (int sg = 0; sg < nseg2; ++sg) {
-            const int r0 = (int)((int64_t)sg * dh2 / nseg2), r1 = (int)((int64_t)(sg + 1) * dh2 / nseg2);
-            seg2[4 * sg] = h2.vbase[r0] / cho * cho;
+            // segments start on a row pair
+            const int r0 = (int)((int64_t)sg * dh2 / nseg2) & ~1;
+            const int r1 = sg + 1 == nseg2 ? dh2 : (int)((int64_t)(sg + 1) * dh2 / nseg2) & ~1;
+            seg2[4 * sg] = pbase[r0 / 2] / cho * cho;
             seg2[4 * sg + 1] = std::min(cdh1, (need[r1 - 1] / cho + 1) * cho);
             seg2[4 * sg + 2] = r0;
             seg2[4 * sg + 3] = r1;
@@ -1282,6 +1316,14 @@ int launch_chain_planes(pp_scale_plan *P, const pp::PlaneJob *const *jobs, const
 // the plain first-stage plan, then the chroma planes' chain launch
 int launch_chain(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, int nframes, hipStream_t st) {
     using namespace pp;
+    if (P->luma && P->luma->fast_hw == P->fast_hw && PP_KNOB("PIXPATH_CHAIN_COMBINED")) {
+        // measurement: the luma plan's job (32-row chunks) and the chroma
+        // chain jobs in ONE launch, LDS the larger of the two layouts
+        const PlaneJob *jobs[3] = {&P->luma->fjob[0], &P->fjob[1], &P->fjob[2]};
+        const int pl[3] = {0, 1, 2};
+        return launch_chain_planes(P, jobs, pl, 3, P->fast_hw, std::max(P->luma->fast_lds_plane[0], P->chain_lds), src,
+                                   dst, nframes, st);
+    }
     if (P->luma) {
         // PIXPATH_CHAIN_OVERLAP (measurement build): the luma launch on a side
         // stream, concurrent with the chroma launch (fork / join events on `st`)

@@ -539,29 +539,35 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                 __syncthreads();  // this chunk's first-stage rows are in ring2
                 const int lo2 = max(chunk2[4 * ci], r2lo), hi2 = min(chunk2[4 * ci + 1], r2hi);
                 const kconst int32_t *vrow2 = as_kconst<int32_t>(J.vrow2);
-                // VT2 tap pairs compile-time; the row records of G2 rows come
-                // through the scalar cache at once (as in the first stage's V
-                // pass: one exposed scalar-load latency per group, not per row)
+                // rows in pairs (2m, 2m + 1): the vertical 4:2:0 -> 4:2:2 step is
+                // a 2x upsample, so both rows of a pair read one window of ring2
+                // rows (record [m][16]: base row, VT2 taps of row 2m, VT2 of
+                // row 2m + 1, zero outside each row's own taps) -- the rows are
+                // read and interleaved into v_dot2 pairs once for two output rows.
+                // The records of G2 pairs come through the scalar cache at once.
                 auto pass2 = [&](auto vt_c, auto cl_c) {
                     constexpr int VT2 = decltype(vt_c)::value;
                     constexpr bool CL = decltype(cl_c)::value;
                     const int vx = CL ? cxv : cx, vxo = CL ? xov : xo;
-                    constexpr int G2 = 4;
-                    for (int g0 = lo2 + rg; g0 < hi2; g0 += 4 * G2) {
+                    constexpr int G2 = 2;
+                    const int m_lo = lo2 >> 1, m_hi = (hi2 + 1) >> 1;
+                    for (int g0 = m_lo + rg; g0 < m_hi; g0 += 4 * G2) {
                         int vb[G2];
-                        int32_t cf[G2][VT2];
+                        int32_t cf[G2][2][VT2];
 #pragma unroll
                         for (int i = 0; i < G2; ++i) {
-                            const kconst int32_t *row = vrow2 + (int64_t)min(g0 + 4 * i, hi2 - 1) * 16;
+                            const kconst int32_t *row = vrow2 + (int64_t)min(g0 + 4 * i, m_hi - 1) * 16;
                             vb[i] = row[0];
 #pragma unroll
-                            for (int j = 0; j < VT2; ++j) cf[i][j] = row[1 + j];
+                            for (int j = 0; j < VT2; ++j) {
+                                cf[i][0][j] = row[1 + j];
+                                cf[i][1][j] = row[1 + VT2 + j];
+                            }
                         }
 #pragma unroll
                         for (int i = 0; i < G2; ++i) {
-                            const int r2 = g0 + 4 * i;
-                            if (r2 >= hi2) break;
-                            int acc[4];
+                            const int m = g0 + 4 * i;
+                            if (m >= m_hi) break;
                             // rows vb + 2j, vb + 2j + 1 from the byte ring, interleaved into
                             // the (row, row + 1) sample pairs of v_dot2; the first stage's
                             // << 7 (hScale8To15 of the identity H filter) moves onto the sum
@@ -571,42 +577,44 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                                 ra[j] = *reinterpret_cast<const uint32_t *>(ring2b + ((vb[i] + 2 * j) & J.r2mask) * TW + vx);
                                 rb[j] = *reinterpret_cast<const uint32_t *>(ring2b + ((vb[i] + 2 * j + 1) & J.r2mask) * TW + vx);
                             }
-                            uint4 q[VT2];
+                            int acc2[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll
-                            for (int j = 0; j < VT2; ++j) {
-                                q[j].x = __builtin_amdgcn_perm(rb[j], ra[j], 0x0c040c00u);
-                                q[j].y = __builtin_amdgcn_perm(rb[j], ra[j], 0x0c050c01u);
-                                q[j].z = __builtin_amdgcn_perm(rb[j], ra[j], 0x0c060c02u);
-                                q[j].w = __builtin_amdgcn_perm(rb[j], ra[j], 0x0c070c03u);
+                            for (int j = 0; j < VT2; ++j) {  // interleave once, accumulate both rows
+                                const uint32_t q[4] = {__builtin_amdgcn_perm(rb[j], ra[j], 0x0c040c00u),
+                                                       __builtin_amdgcn_perm(rb[j], ra[j], 0x0c050c01u),
+                                                       __builtin_amdgcn_perm(rb[j], ra[j], 0x0c060c02u),
+                                                       __builtin_amdgcn_perm(rb[j], ra[j], 0x0c070c03u)};
+#pragma unroll
+                                for (int h = 0; h < 2; ++h) {
+                                    const v2i16 c2 = __builtin_bit_cast(v2i16, cf[i][h][j]);
+#pragma unroll
+                                    for (int e = 0; e < 4; ++e)
+                                        acc2[h][e] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[e]), c2, acc2[h][e], false);
+                                }
                             }
 #pragma unroll
-                            for (int j = 0; j < 4; ++j) acc[j] = 0;
+                            for (int h = 0; h < 2; ++h) {
+                                const int r2 = 2 * m + h;
+                                int acc[4];
 #pragma unroll
-                            for (int j = 0; j < VT2; ++j) {
-                                const v2i16 c2 = __builtin_bit_cast(v2i16, cf[i][j]);
-                                acc[0] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].x), c2, acc[0], false);
-                                acc[1] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].y), c2, acc[1], false);
-                                acc[2] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].z), c2, acc[2], false);
-                                acc[3] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].w), c2, acc[3], false);
+                                for (int j = 0; j < 4; ++j)
+                                    acc[j] = (acc2[h][j] << 7) + (FUSE == 8 ? 64 << 12 : 1 << (10 + 16 - FUSE));
+                                if ((!CL && !lane_any) || r2 >= hi2) continue;
+                                constexpr int s2 = FUSE == 8 ? 19 : 11 + 16 - FUSE;
+                                int w[4];
+#pragma unroll
+                                for (int j = 0; j < 4; ++j) w[j] = min(max(acc[j] >> s2, 0), (1 << FUSE) - 1);
+                                store4<FUSE>(dbase + (int64_t)r2 * dls, vxo, w, CL || (lane_full && a.vec_dst), jdw);
                             }
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) acc[j] = (acc[j] << 7) + (FUSE == 8 ? 64 << 12 : 1 << (10 + 16 - FUSE));
-                            if (!CL && !lane_any) continue;
-                            constexpr int s2 = FUSE == 8 ? 19 : 11 + 16 - FUSE;
-                            int w[4];
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) w[j] = min(max(acc[j] >> s2, 0), (1 << FUSE) - 1);
-                            store4<FUSE>(dbase + (int64_t)r2 * dls, vxo, w, CL || (lane_full && a.vec_dst), jdw);
                             __builtin_amdgcn_sched_barrier(0);
                         }
                     }
                 };
                 auto dispatch2 = [&](auto cl_c) {
-                    switch (J.vtp2) {  // uniform; the host allows <= 4 pairs
+                    switch (J.vtp2) {  // uniform; the host allows <= 3 pairs (a row pair's window)
                     case 1: pass2(std::integral_constant<int, 1>{}, cl_c); break;
                     case 2: pass2(std::integral_constant<int, 2>{}, cl_c); break;
-                    case 3: pass2(std::integral_constant<int, 3>{}, cl_c); break;
-                    default: pass2(std::integral_constant<int, 4>{}, cl_c); break;
+                    default: pass2(std::integral_constant<int, 3>{}, cl_c); break;
                     }
                 };
                 if constexpr (strip_clamp_path<ST, OUTB, HW, VTM, FUSE>()) {
