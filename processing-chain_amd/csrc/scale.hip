@@ -443,7 +443,7 @@ struct pp_scale_plan {
     // takes the 16-row chunks and ring2 LDS the chroma planes need
     pp_scale_plan *luma = nullptr;
     size_t fast_lds_plane[2] = {0, 0};  // strip_kernel LDS of the luma / chroma jobs alone
-    size_t fast_lds_direct = 0;         // strip_kernel DIRECT instances (8-bit source, HW 8): the V window ring only
+    bool direct = false;                // strip_kernel DIRECT tiling (8-bit source, HW 8): fast_lds = the V ring only
     std::vector<int32_t> chroma_lo, chroma_hi;  // chain first stage: source rows of each chroma chunk (host copy)
     hipStream_t side = nullptr;       // CHAIN with `luma`: the luma launch's stream when the two launches overlap
     hipEvent_t fork = nullptr, join = nullptr;
@@ -563,7 +563,7 @@ static size_t lds_budget() {
 // Strip width / chunk height / segments for one plane: the widest strip and
 // tallest chunk whose LDS (staging + ring) fits the budget; ~256-row segments.
 int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::string *err, int seg_force = 0,
-               int cho_force = 0) {
+               int cho_force = 0, bool ring_only = false) {
     static const int tws[] = {256, 128, 64, 32};
     static const int chos[] = {64, 48, 32, 24, 16, 8, 4, 2, 1};
     // tuning overrides (measurement only): tallest chunk, rows per segment
@@ -581,8 +581,10 @@ int plan_tiles(HostPlane &hp, int sw, int sh, int dw, int dh, size_t *lds, std::
             nseg = (dh + seg_h - 1) / seg_h;
             int maxnew, ring;
             row_chunks(hp, sh, dh, cho, seg_h, &maxnew, &ring);
-            const size_t bytes = (size_t)maxnew * S * 2 + (size_t)ring * tw * 2 +
-                                 (size_t)cho * hp.vtp * 4 + (size_t)cho * 4;
+            // ring_only: strip_kernel DIRECT, whose LDS is the V window ring alone
+            const size_t bytes = ring_only ? (size_t)ring * tw * 2
+                                           : (size_t)maxnew * S * 2 + (size_t)ring * tw * 2 + (size_t)cho * hp.vtp * 4 +
+                                                 (size_t)cho * 4;
             if (bytes > lds_budget()) continue;
             hp.tiles_x = (dw + tw - 1) / tw;
             hp.nseg = nseg; hp.tw = tw; hp.seg_h = seg_h; hp.cho = cho;
@@ -671,10 +673,15 @@ inline int hw_bucket(int need) {
 
 }  // namespace
 
+#ifndef PIXPATH_DIRECT_CHO
+#define PIXPATH_DIRECT_CHO 24
+#endif
+constexpr int kDirectCho = PIXPATH_DIRECT_CHO;  // strip_kernel DIRECT: tallest chunk (output rows)
+
 // one_seg_chroma: chroma planes walk their whole height in one segment (the
 // chain plan's second-stage vertical filter follows the first stage's rows)
 static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, int dw, int dh, int flags, double p0,
-                       double p1, bool one_seg_chroma, pp_scale_plan **out, int cho_max = 0) {
+                       double p1, bool one_seg_chroma, pp_scale_plan **out, int cho_max = 0, bool allow_direct = true) {
     using namespace pp;
     if (!out) PP_FAIL(PP_ERR_INVALID, "null argument");
     *out = nullptr;  // ctx == NULL: host-only plan (tables for introspection, no device upload)
@@ -777,7 +784,6 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
                 hp[c].S_fast = std::max(hp[c].f_S, (hp[c].max_base + 2 * HW + 15) & ~15);
                 P->fast_lds_plane[c] = (size_t)hp[c].maxnew * hp[c].S_fast * 2 + (size_t)hp[c].ring * ftw * 2;
                 lds = std::max(lds, P->fast_lds_plane[c]);
-                P->fast_lds_direct = std::max(P->fast_lds_direct, (size_t)hp[c].ring * ftw * 2);
             }
             if (HW > 0 && lds <= lds_budget() * (size_t)(ftw / 256)) {
                 P->fast_hw = HW;
@@ -785,6 +791,28 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
                 P->fast_tw = ftw;
                 break;
             }
+        }
+    }
+
+    // strip_kernel DIRECT (8-bit sources, 8-dword windows, plain plans: the
+    // 2:1 downscales of config 3): no staged rows, so the chunks are chosen
+    // for the V window ring alone -- its own row tiling and chunk tables
+    // (24-row chunks: 2.73 ms per 600-frame config-3 8-bit launch, against
+    // 3.04 at the staged plan's 8 rows and 2.76 at 32, profiles/r5/)
+    HostPlane hpd[2];
+    if (P->fast_hw == 8 && si.depth == 8) {
+        bool okd = allow_direct && !di.packed && !one_seg_chroma && P->fast_tw == 256;
+        size_t dl = 0;
+        for (int c = 0; c < 2 && okd; ++c) {
+            hpd[c] = hp[c];
+            size_t tmp = 0;
+            okd = plan_tiles(hpd[c], c ? P->csw : sw, c ? P->csh : sh, c ? P->cdw : dw, c ? P->cdh : dh, &tmp, &err, 0,
+                             kDirectCho, true) == 0 && hpd[c].tw == 256;
+            dl = std::max(dl, (size_t)hpd[c].ring * 256 * 2);
+        }
+        if (okd) {
+            P->direct = true;
+            P->fast_lds = dl;
         }
     }
 
@@ -816,6 +844,10 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
                 F.tw = P->fast_tw;
                 F.twl = P->fast_tw == 512 ? 9 : 8;
             }
+            if (P->direct) {
+                F.tiles_y = hpd[c].nseg; F.seg_h = hpd[c].seg_h; F.cho = hpd[c].cho;
+                F.ring = hpd[c].ring; F.maxnew = 0;
+            }
             F.tile_base = fbase;
             fbase += F.tiles_x * F.tiles_y;
         }
@@ -837,12 +869,12 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
         total += sz4(hp[c].h.pos.size()) + sz2(hp[c].h.coef.size()) + sz4(hp[c].vbase.size()) +
                  sz4(hp[c].vcoef2.size()) + 2 * sz4(hp[c].c0.size()) + 2 * sz4(hp[c].lo.size()) +
                  sz4(hp[c].hbase4.size()) + sz4(hp[c].hcoefw.size()) + sz4(hp[c].vrow16.size()) +
-                 sz4(hp[c].f_c0.size()) + sz4(hp[c].f_cn.size());
+                 sz4(hp[c].f_c0.size()) + sz4(hp[c].f_cn.size()) + 2 * sz4(hpd[c].lo.size());
     PP_HIP(hipSetDevice(ctx->device));
     PP_HIP(hipMalloc(&P->dev, total));
     std::vector<uint8_t> host(total, 0);
     size_t off = 0;
-    const int32_t *dptr32[2][12] = {};
+    const int32_t *dptr32[2][14] = {};
     const int16_t *dptr16[2][1];
     auto put = [&](const void *src, size_t bytes, size_t padded) {
         std::memcpy(host.data() + off, src, bytes);
@@ -866,6 +898,10 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
             dptr32[c][10] = (const int32_t *)put(hp[c].f_c0.data(), hp[c].f_c0.size() * 4, sz4(hp[c].f_c0.size()));
             dptr32[c][11] = (const int32_t *)put(hp[c].f_cn.data(), hp[c].f_cn.size() * 4, sz4(hp[c].f_cn.size()));
         }
+        if (P->direct) {
+            dptr32[c][12] = (const int32_t *)put(hpd[c].lo.data(), hpd[c].lo.size() * 4, sz4(hpd[c].lo.size()));
+            dptr32[c][13] = (const int32_t *)put(hpd[c].hi.data(), hpd[c].hi.size() * 4, sz4(hpd[c].hi.size()));
+        }
     }
     PP_HIP(hipMemcpy(P->dev, host.data(), total, hipMemcpyHostToDevice));
 
@@ -883,6 +919,10 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
         F.hbase4 = J.hbase4; F.hcoefw = J.hcoefw; F.vrow16 = J.vrow16;
         F.tile_c0 = P->fast_hw ? dptr32[c][10] : J.tile_c0;
         F.tile_cn = P->fast_hw ? dptr32[c][11] : J.tile_cn;
+        if (P->direct) {
+            F.chunk_lo = dptr32[c][12];
+            F.chunk_hi = dptr32[c][13];
+        }
     }
     *out = P.release();
     return PP_OK;
@@ -937,7 +977,7 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
     // 16-row chunks: the LDS ring of the second stage then still leaves 6
     // workgroups per CU (32-row chunks: 2.73 vs 2.30 ms per 600-frame config-4
     // canvas launch, profiles/r2/chain_ab.log)
-    int rc = plan_create(ctx, src_fmt, sw, sh, PP_FMT_YUV420P, dw, dh, flags, p0, p1, true, &s1, kChainCho);
+    int rc = plan_create(ctx, src_fmt, sw, sh, PP_FMT_YUV420P, dw, dh, flags, p0, p1, true, &s1, kChainCho, false);
     if (rc) return rc;
     std::unique_ptr<pp_scale_plan> P(s1);
     rc = plan_create(ctx, PP_FMT_YUV420P, dw, dh, dst_fmt, dw, dh, PP_SWS_BICUBIC, PP_SWS_PARAM_DEFAULT,
@@ -1071,7 +1111,8 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
     // only the ring2 planes): its plan is the plain first stage, same filters
     pp_scale_plan *lp = nullptr;
     // PIXPATH_CHAIN_ONE_LAUNCH (measurement build): keep luma in the chroma launch
-    if (v422 && !PP_KNOB("PIXPATH_CHAIN_ONE_LAUNCH") && plan_create(ctx, src_fmt, sw, sh, PP_FMT_YUV420P, dw, dh, flags, p0, p1, false, &lp) == PP_OK) {
+    if (v422 && !PP_KNOB("PIXPATH_CHAIN_ONE_LAUNCH") &&
+        plan_create(ctx, src_fmt, sw, sh, PP_FMT_YUV420P, dw, dh, flags, p0, p1, false, &lp, 0, false) == PP_OK) {
         if (lp->kind == pp_scale_plan::GENERIC && lp->fast_hw > 0 && lp->fast_tw == 256) {
             P->luma = lp;
             lp->fjob[0].fuse = P->chain_out > 8 ? 1 : 0;
@@ -1191,7 +1232,9 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
     KernelFn k;
     size_t lds = P->lds_bytes;
     int tiles = P->job[2].tile_base + P->job[2].tiles_x * P->job[2].tiles_y, threads = kThreads;
-    if (P->fast_hw && a.vec_src) {
+    // (an 8-bit HW-8 plan takes the strip path only with its DIRECT tiling:
+    // that instance stages no rows)
+    if (P->fast_hw && a.vec_src && (P->direct || !(P->si.depth == 8 && P->fast_hw == 8))) {
         for (int p = 0; p < 3; ++p) a.pl[p] = P->fjob[p];
         lds = P->fast_lds;
         tiles = P->fast_tiles;
@@ -1199,10 +1242,7 @@ int launch_generic(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst,
         const int vtm = strip_vtm_bucket(std::max(P->fjob[0].vtp, P->fjob[1].vtp));
         k = P->si.depth == 8 ? pick_strip_u8(out_depth, P->fast_hw, vtm, P->fast_tw)
                              : pick_strip_u16(out_depth, P->fast_hw, vtm, P->fast_tw);
-        if (P->si.depth == 8 && P->fast_hw == 8) {  // strip_kernel DIRECT: no staged rows in LDS
-            for (int p = 0; p < 3; ++p) a.pl[p].maxnew = 0;
-            lds = P->fast_lds_direct;
-        }
+
     } else if (P->si.depth == 8) {
         k = out_depth == 8 ? pick_ht<uint8_t, 8>(P->ht, tw256) : pick_ht<uint8_t, 10>(P->ht, tw256);
     } else {

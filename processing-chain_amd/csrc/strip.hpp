@@ -139,11 +139,13 @@ constexpr bool strip_clamp_path() {
 template <typename ST, int OUTB, int HW, int VTM, int FUSE = 0, int TW = 256>
 __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() : strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
     static_assert(TW == 256 || TW == 512, "strip width");
-    // DIRECT (8-bit sources, 8-dword windows: the 2:1 downscales of config 3):
-    // no staged source rows -- a lane loads its window's 16 source bytes of a
-    // row straight into registers for the H pass, so the plan's LDS is the V
-    // window ring alone (the staged rows, widened to 16 bits, were two thirds
-    // of it and kept the chunks at 8 rows)
+    // DIRECT (8-dword windows: the 2:1 downscales of config 3): no staged
+    // source rows -- a lane loads its window's 16 source samples of a row
+    // straight into registers for the H pass (one 16-B load of 8-bit samples,
+    // two of 16-bit ones), so the plan's LDS is the V window ring alone (the
+    // staged rows were two thirds of it and kept the chunks at 8 rows).
+    // 8-bit sources only: config 3's 10-bit source measured slower direct
+    // (4.85 vs 4.73 ms at 24-row chunks, profiles/r5/config3_direct.txt)
     constexpr bool DIRECT = sizeof(ST) == 1 && HW == 8 && FUSE == 0;
     extern __shared__ __align__(16) uint16_t lds[];
     const int L = xcd_remap(blockIdx.x, gridDim.x);
@@ -320,19 +322,35 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
         // ---- horizontal pass: row pairs of the window, wave-strided ----------
         if (nnew > 0 && (PP_ABLATE(a.debug) & 4)) next_src = hi;
         if (DIRECT && nnew > 0 && !(PP_ABLATE(a.debug) & 4)) {
-            // window row i = source row base + i; a lane's 16 bytes at its
+            // window row i = source row base + i; a lane's 16 samples at its
             // window base (dword aligned: c0 % 16 == 0, hb % 4 == 0)
             const int i0 = next_src - base;
             const int kf0 = (i0 + 1) >> 1, kf1 = (i0 + nnew) >> 1;
-            const int hoff = cbyte + hb;
-            auto ld = [&](int i) { return bload16(rs, (base + i) * (int)sls + hoff); };
-            auto hregs = [&](const uint4 r, int out[4]) {  // hrow4 on register-held bytes
-                const uint32_t d4[4] = {r.x, r.y, r.z, r.w};
-                uint32_t w[HW];
+            const int hoff = cbyte + hb * (int)sizeof(ST);
+            struct Win {
+                uint4 v[sizeof(ST)];
+            };
+            auto ld = [&](int i) {
+                Win r;
+                const int off = (base + i) * (int)sls + hoff;
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    w[2 * m] = __builtin_amdgcn_perm(0u, d4[m], 0x0c010c00u);
-                    w[2 * m + 1] = __builtin_amdgcn_perm(0u, d4[m], 0x0c030c02u);
+                for (int k = 0; k < (int)sizeof(ST); ++k) r.v[k] = bload16(rs, off + 16 * k);
+                return r;
+            };
+            auto hregs = [&](const Win &r, int out[4]) {  // hrow4 on register-held samples
+                uint32_t w[HW];
+                if constexpr (sizeof(ST) == 1) {
+                    const uint32_t d4[4] = {r.v[0].x, r.v[0].y, r.v[0].z, r.v[0].w};
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        w[2 * m] = __builtin_amdgcn_perm(0u, d4[m], 0x0c010c00u);
+                        w[2 * m + 1] = __builtin_amdgcn_perm(0u, d4[m], 0x0c030c02u);
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        w[4 * k] = r.v[k].x; w[4 * k + 1] = r.v[k].y; w[4 * k + 2] = r.v[k].z; w[4 * k + 3] = r.v[k].w;
+                    }
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -344,7 +362,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                     out[j] = acc < 32767 ? acc : 32767;
                 }
             };
-            auto pair_out = [&](int k, const uint4 ra, const uint4 rb) {
+            auto pair_out = [&](int k, const Win &ra, const Win &rb) {
                 int oa[4], ob[4];
                 hregs(ra, oa);
                 hregs(rb, ob);
@@ -371,7 +389,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
             }
             int k = kf0 + rg;
             for (; k + 4 < kf1; k += 8) {  // two pairs a step: four row loads in flight
-                const uint4 a0 = ld(2 * k), a1 = ld(2 * k + 1), b0 = ld(2 * k + 8), b1 = ld(2 * k + 9);
+                const Win a0 = ld(2 * k), a1 = ld(2 * k + 1), b0 = ld(2 * k + 8), b1 = ld(2 * k + 9);
                 pair_out(k, a0, a1);
                 pair_out(k + 4, b0, b1);
             }
