@@ -12,7 +12,22 @@ read side is doubled; WRITE_SIZE is exact for 16-B/lane streaming stores
 import csv
 import collections
 import json
+import os
 import sys
+
+# PIXPATH_TRACE_BY_GRID=1: launches of one kernel with different grid sizes
+# apart (the chain plan's luma and chroma launches of one strip_kernel instance)
+BY_GRID = bool(os.environ.get("PIXPATH_TRACE_BY_GRID"))
+
+
+def _key(short, row):
+    if not BY_GRID:
+        return short
+    g = 1
+    for k, v in row.items():
+        if k.startswith("Grid_Size") and v:
+            g *= int(v)
+    return "%s grid=%d" % (short, g)
 
 KERNELS = {"scale_kernel": "pp::scale_kernel", "strip_kernel": "pp::strip_kernel", "siti_kernel": "pp::siti_kernel", "v210_kernel": "pp::v210_kernel",
            "pad_kernel": "pp::pad_kernel", "stall_kernel": "pp::stall_kernel", "cpvs_kernel": "pp::cpvs_kernel"}
@@ -25,7 +40,7 @@ def per_kernel(path, counter):
             continue
         for short, pat in KERNELS.items():
             if pat in r["Kernel_Name"]:
-                agg[short].append(float(r["Counter_Value"]) * 1024.0)
+                agg[_key(short, r)].append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
@@ -37,7 +52,7 @@ def main():
     for r in csv.DictReader(open(trace_csv)):
         for short, pat in KERNELS.items():
             if pat in r["Kernel_Name"]:
-                dur[short].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                dur[_key(short, r)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     res = {"frames_per_launch": int(frames), "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes)",
            "correction": "read bytes = 2 x FETCH_SIZE (gfx950, MI355X_MICROARCH.md HBM section)", "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
