@@ -796,6 +796,23 @@ extern "C" int pp_ffv1_encoder_create(pp_ctx *ctx, int fmt, int w, int h, int sl
     if (slices_h < 1 || slices_v < 1 || slices_h * slices_v > 256 || slices_h > w / 4 || slices_v > h / 4)
         PP_FAIL(PP_ERR_INVALID, "slice grid %dx%d", slices_h, slices_v);
     if (max_frames < 1) PP_FAIL(PP_ERR_INVALID, "max_frames %d", max_frames);
+    // every chroma sample in some slice: a slice at x0 covers chroma columns
+    // [x0 >> hsub, +ceil((x1 - x0) / 2^hsub)) (RFC 9043 slice geometry), so an
+    // odd boundary can leave the last chroma column / row in no slice -- e.g.
+    // 333x191 4:2:0 in 3x3 slices; FFmpeg's encoder picks other grids
+    // (ff_need_new_slices), this one refuses instead of dropping samples
+    auto covers = [](int n, int ns, int sub) {
+        int end = 0;
+        for (int i = 0; i < ns; ++i) {
+            const int a = (int)((int64_t)i * n / ns), b = (int)((int64_t)(i + 1) * n / ns);
+            if ((a >> sub) > end) return false;
+            end = std::max(end, (a >> sub) + (((b - a) + (1 << sub) - 1) >> sub));
+        }
+        return end >= ((n + (1 << sub) - 1) >> sub);
+    };
+    if (!covers(w, slices_h, fi.hsub) || !covers(h, slices_v, fi.vsub))
+        PP_FAIL(PP_ERR_UNSUPPORTED, "slice grid %dx%d leaves chroma samples of a %dx%d frame in no slice", slices_h,
+                slices_v, w, h);
     std::unique_ptr<pp_ffv1_enc> E(new pp_ffv1_enc());
     E->ctx = ctx; E->fmt = fmt; E->w = w; E->h = h; E->nh = slices_h; E->nv = slices_v; E->fi = fi;
     E->max_frames = max_frames;

@@ -91,3 +91,14 @@ def test_decoder_geometry_fits_the_lds(w, grid, lpw, cap):
     dec = ffv1.Ffv1Decoder(x, w, 64, host_only=True)
     assert (dec.slices_per_workgroup, dec.row_cap) == (lpw, cap)
     assert 2560 + lpw * cap * 2 <= 160 * 1024 - 4096
+
+
+def test_encoder_refuses_grids_that_drop_chroma():
+    """A slice at x0 covers chroma columns [x0 >> hsub, + ceil(width / 2)): with
+    odd slice boundaries the last chroma row / column can fall in no slice
+    (333x191 4:2:0 in 3x3 slices misses chroma row 95).  FFmpeg's encoder
+    avoids such grids; pixpath's refuses them instead of dropping samples."""
+    with pytest.raises(Exception, match="no slice"):
+        ffv1.Ffv1Encoder("yuv420p", 333, 191, slices=(3, 3), host_only=True)
+    ffv1.Ffv1Encoder("yuv422p", 333, 191, slices=(3, 3), host_only=True)   # no vertical subsampling
+    ffv1.Ffv1Encoder("yuv420p", 333, 190, slices=(3, 2), host_only=True)   # odd width, covered

@@ -139,3 +139,20 @@ def test_reference_made_avpvs_routes_to_the_gpu_decoder(gpu, tmp_path):
     for j in (0, 13, n - 1):
         want = po.v210_pack(po.pad(po.YUV422P10LE, frames[j], 640, 400, 0, 20))
         np.testing.assert_array_equal(raw[j * fb:(j + 1) * fb], want.reshape(-1))
+
+
+@pytest.mark.parametrize("fmt,fid,bits,hs,vs,w,h,grid", [
+    ("yuv420p", po.YUV420P, 8, 1, 1, 333, 190, (3, 2)),        # ragged: odd width, unequal slices
+    ("yuv422p10le", po.YUV422P10LE, 10, 1, 0, 250, 66, (4, 1)),
+    ("yuv444p10le", po.YUV444P10LE, 10, 0, 0, 320, 176, (2, 2)),  # 4:4:4 (FFmpeg's ffv1 writes it too)
+    ("yuv444p", po.YUV444P, 8, 0, 0, 96, 40, (1, 1))])
+def test_ragged_and_444_streams(gpu, fmt, fid, bits, hs, vs, w, h, grid):
+    """Odd frame sizes (chroma planes rounded up, slices of unequal width, a
+    chroma column two slices share) and 4:4:4 chroma, GOP 5 with states
+    carried: every frame exact."""
+    from pixpath import ffv1
+    pf = ffmpeg_like(bits, hs, vs, *grid, gop=5)
+    frames, pkts = _sequence(pf, fid, w, h, 11, w + h)
+    dec = ffv1.Ffv1Decoder(ref.gen_extradata(pf), w, h, max_frames=11, device=gpu)
+    assert dec.fmt.name == fmt
+    _check(dec.decode(b"".join(pkts), [len(p) for p in pkts]).to_numpy(), frames)
