@@ -545,11 +545,13 @@ def cmd_stall(args):
 
 def cmd_concat(args):
     """create_avpvs_long_concat (lib/ffmpeg.py:1058-1105: `ffmpeg -f concat
-    -safe 0 -i <filelist> -c:v copy -t <total>`) for GPU-FFV1 AVIs: the
-    segment canvases' packets copied in filelist order (all-intra FFV1, one
-    configuration record), cut after round(total * rate) frames.  No pixels
-    are decoded."""
+    -safe 0 -i <filelist> -c:v copy -t <total>`) for FFV1 AVIs of one
+    configuration record: the segment canvases' packets copied in filelist
+    order, each with its keyframe flag (an FFmpeg-made GOP stream's inter
+    frames are not marked key in the index), cut after round(total * rate)
+    frames.  No pixels are decoded."""
     from . import avi
+    from .ffv1 import packet_is_keyframe
     out = args.output
     if _skip(out, args.y):
         return 0
@@ -577,7 +579,8 @@ def cmd_concat(args):
                     if cap is not None and n >= cap:
                         break
                     fh.seek(off)
-                    wr.write_packet(fh.read(size))
+                    pkt = fh.read(size)
+                    wr.write_packet(pkt, key=packet_is_keyframe(pkt))
                     n += 1
     except BaseException:
         wr.abort()

@@ -669,6 +669,14 @@ def is_pixpath_ffv1(info):
     return probe.extradata == info["extradata"]
 
 
+def packet_is_keyframe(pkt):
+    """The keyframe flag of an FFV1 frame packet: the first decision of its
+    first slice's range coder at state 128 (ffv1dec.c decode_frame), i.e. the
+    first two bytes as a 16-bit value (clamped to 0xFF00) >= 0x7F80."""
+    low = (pkt[0] << 8) | pkt[1] if len(pkt) >= 2 else 0
+    return min(low, 0xFF00) >= 0x7F80
+
+
 def gpu_decodable(info):
     """True when the GPU decoder reads an AVI's video stream (avi.scan info):
     FFV1 whose configuration record pp_ffv1_decoder_create accepts -- pixpath's

@@ -165,3 +165,53 @@ def test_product_parser_refuses_corrupt_records():
             ffv1.Ffv1Decoder(bytes(bad), 640, 360, host_only=True)
     with pytest.raises(Exception):
         ffv1.Ffv1Decoder(x[:12], 640, 360, host_only=True)
+
+
+def test_keyframe_flag_from_the_packet():
+    """packet_is_keyframe reads the frame coder's first decision (what the
+    decoder's host side uses to cut GOPs, ffv1host.cpp ffv1_keyframe_bit):
+    true exactly on the GOP's first frames of an FFmpeg-like stream and on
+    every frame of pixpath's intra stream."""
+    from pixpath.ffv1 import packet_is_keyframe
+    rng = np.random.default_rng(4)
+    w, h = 96, 64
+    pf = ffmpeg_like(8, 1, 1, gop=4)
+    enc = ref.GenEncoder(pf, w, h)
+    keys = [packet_is_keyframe(enc.encode(f)) for f in _frames(rng, po.YUV420P, w, h, 9)]
+    assert keys == [i % 4 == 0 for i in range(9)]
+    f = synth.noise_frame(rng, po.YUV420P, w, h)
+    assert packet_is_keyframe(ref.encode_frame(f, 8, 1, 1, 2, 2))
+
+
+def test_concat_keeps_gop_keyframe_flags(tmp_path):
+    """`cli concat` of FFmpeg-like GOP segment AVIs (create_avpvs_long_concat's
+    packet copy): packets byte for byte, the index's keyframe flags from the
+    packets."""
+    import struct
+    from pixpath import avi, cli
+    rng = np.random.default_rng(6)
+    w, h = 96, 64
+    pf = ffmpeg_like(10, 1, 0, gop=3)
+    x = ref.gen_extradata(pf)
+    segs, allp = [], []
+    for k in range(2):
+        enc = ref.GenEncoder(pf, w, h)
+        pk = [enc.encode(f) for f in _frames(rng, po.YUV422P10LE, w, h, 5)]
+        path = str(tmp_path / ("seg%d.avi" % k))
+        wr = avi.AviWriter(path, w, h, 60, extradata=x)
+        for i, p in enumerate(pk):
+            wr.write_packet(p, key=i % 3 == 0)
+        wr.close()
+        segs.append(path)
+        allp += pk
+    fl = tmp_path / "list.txt"
+    fl.write_text("".join("file '%s'\n" % s for s in segs))
+    out = str(tmp_path / "long.avi")
+    assert cli.main(["concat", "-y", "--filelist", str(fl), out]) == 0
+    info, pk = avi.read_packets(out)
+    assert pk == allp and info["extradata"] == x
+    data = open(out, "rb").read()
+    i = data.index(b"idx1")
+    n = struct.unpack_from("<I", data, i + 4)[0] // 16
+    flags = [struct.unpack_from("<4sIII", data, i + 8 + 16 * j)[1] for j in range(n)]
+    assert [bool(f & 0x10) for f in flags] == [j % 5 % 3 == 0 for j in range(10)]
