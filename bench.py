@@ -941,9 +941,70 @@ def bench_ffv1(args, rank, world, dev):
         out["cpu_baseline"] = {"value": round(k / cdt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
                                "sample": "%d frames through oracle/ffv1_oracle.c (gcc -O3, one thread)" % k,
                                "cpu_model": host_cpu()[0]}
+        out["reference_stream_decode"] = reference_stream_decode(args, src, dev, ffv1_ref)
     if rank == 0:
         print(json.dumps(out), flush=True)
     return 0
+
+
+def reference_stream_decode(args, src, dev, ffv1_ref):
+    """GPU decode of an AVPVS in the reference's own FFV1 shape
+    (`-threads 4 -level 3 -coder 1 -context 1`, /root/reference/lib/ffmpeg.py:993:
+    2x2 slices, -context 1's 5-input set, a transmitted state table, GOPs of 12
+    with states carried).  The oracle's general encoder writes one GOP of the
+    bench content (input generation, untimed; FFmpeg is absent); the GPU decodes
+    that GOP repeated 50 times (600 frames = 200 slice chains, one lane each),
+    checked lossless; the oracle's own decode of the GOP is the CPU row.  A
+    chain is one slice over a whole GOP, so this stream has 200 serial chains
+    where pixpath's 8x8 intra stream has 38,400."""
+    import time
+    import numpy as np
+    import torch
+    from pixpath import ffv1
+    from pixpath.frames import FrameBatch
+    w, h, n, gop = src.w, src.h, src.n, 12
+    reps = n // gop
+    if reps < 1:
+        return None
+    sets = ffv1_ref.ffmpeg_context1_sets(10)
+    pf = ffv1_ref.make_prof(10, 1, 0, 2, 2, sets, tidx=(1, 1), coder=2, gop=gop)
+    frames = [[src.view(p)[f].cpu().numpy() for p in range(3)] for f in range(gop)]
+    genc = ffv1_ref.GenEncoder(pf, w, h)
+    pkts = [genc.encode(f) for f in frames]
+    extra = ffv1_ref.gen_extradata(pf)
+    gdec = ffv1_ref.GenDecoder(extra, w, h)
+    t0 = time.perf_counter()
+    cpu_ok = True
+    for f, p in zip(frames, pkts):
+        rc, planes, _ = gdec.decode(p)
+        cpu_ok = cpu_ok and rc == 0 and all(np.array_equal(planes[q], f[q]) for q in range(3))
+    cdt = time.perf_counter() - t0
+    m = reps * gop
+    one = np.frombuffer(b"".join(pkts), np.uint8)
+    data = torch.from_numpy(np.tile(one, reps)).pin_memory().numpy()
+    sizes = np.tile(np.array([len(p) for p in pkts], np.int64), reps)
+    dec = ffv1.Ffv1Decoder(extra, w, h, max_frames=m, device=dev)
+    back = FrameBatch("yuv422p10le", w, h, m, device=dev)
+    dec.decode(data, sizes, dst=back)  # warm-up
+    torch.cuda.synchronize()
+    steps = max(1, min(args.steps, 2))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        dec.reset()
+        dec.decode(data, sizes, dst=back)
+    torch.cuda.synchronize()
+    ddt = (time.perf_counter() - t0) / steps
+    ok = all(bool(torch.equal(back.view(p)[r * gop:(r + 1) * gop], src.view(p)[:gop]))
+             for p in range(3) for r in (0, reps - 1))
+    return {"frames_per_s": round(m / ddt, 1), "ms_per_step": round(ddt * 1e3, 3), "frames": m, "lossless": ok,
+            "slices": [2, 2], "gop": gop, "chains": reps * 4, "slices_per_workgroup": dec.slices_per_workgroup,
+            "bytes_per_frame": round(len(one) / gop, 1),
+            "cpu_oracle": {"frames_per_s": round(gop / cdt, 3), "cores": 1, "lossless": cpu_ok,
+                           "sample": "one GOP of %d frames, oracle/ffv1_oracle.c general decoder" % gop},
+            "note": "oracle-encoded GOP (FFmpeg's -coder 1 -context 1 shape) repeated %dx; "
+                    "packets from pinned host memory (H2D included); FFmpeg's own files unpinned" % reps}
+
+
 
 
 if __name__ == "__main__":

@@ -29,8 +29,9 @@
  * so decoded pixels are unaffected; the bitstream bytes differ):
  *   - coder_type 1 (range coder, default state table) instead of FFmpeg's
  *     transmitted custom table (coder_type 2, ver2_state -- not available here);
- *   - one quantization table set of 3 inputs, q(d) = min(5, bitlength|d|)
- *     (11 x 11 x 11 -> 666 contexts) instead of -context 1's 5-input set;
+ *   - one quantization table set of 3 inputs, a threshold quantiser per
+ *     bit depth (oracle_quant: 63 contexts at 10 bits, 172 at 8) instead of
+ *     -context 1's 5-input set;
  *   - every frame a keyframe (intra = 1; FFmpeg's default GOP of 12 carries
  *     context state from frame to frame, which would serialise frames);
  *   - num_h_slices x num_v_slices chosen by the caller (FFmpeg: 2 x 2 for
@@ -41,7 +42,7 @@
 #include <string.h>
 
 #define CTX_SIZE 32
-#define NCTX 666  /* (11 * 11 * 11 + 1) / 2 */
+#define NCTX 666  /* (11 * 11 * 11 + 1) / 2: the most contexts a pixpath quantiser has */
 
 /* ---- range coder (rangecoder.c) ---------------------------------------- */
 typedef struct {
@@ -242,23 +243,41 @@ static void put_be32(uint8_t *p, uint32_t v) {
     p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
 }
 
-/* ---- quantisation: q(d) = min(5, bitlength |d|) on (d & 0xFF) as int8 --- */
-int ffv1o_quant(int i /* 0..255 */) {
-    if (i < 128) {
-        int q = 0;
-        while (i) { q++; i >>= 1; }
-        return q < 5 ? q : 5;
-    }
-    return -ffv1o_quant(i == 128 ? 127 : 256 - i);  /* read_quant_table mirrors 128 from 127 */
+/* ---- quantisation (ffv1host.cpp Ffv1Quant): the level of |d| is the number
+ * of thresholds <= |d|, on (d & 0xFF) as int8.  The thresholds the encoder
+ * uses for a bit depth (ffv1host.cpp ffv1_default_quant): */
+typedef struct { int n, thr[5]; } Quant;
+static Quant oracle_quant(int bits) {
+    /* 10 bits: thresholds 4, 32 (5 levels, 63 contexts); 8 bits: 1, 3, 8
+     * (7 levels, 172 contexts).  Round 4's encoder used 1, 2, 4, 8, 16 =
+     * min(5, bit length |d|) (11 levels, 666 contexts) at every depth. */
+    Quant q10 = {2, {4, 32}}, q8 = {3, {1, 3, 8}};
+    return bits > 8 ? q10 : q8;
 }
+static int levels(const Quant *q) { return 2 * q->n + 1; }
+
+static int quant_q(const Quant *q, int i /* 0..255 */) {
+    if (i < 128) {
+        int lv = 0;
+        for (int k = 0; k < q->n; k++) lv += i >= q->thr[k];
+        return lv;
+    }
+    return -quant_q(q, i == 128 ? 127 : 256 - i);  /* read_quant_table mirrors 128 from 127 */
+}
+/* the 8-bit / 10-bit encoder's first quantiser level of d & 0xFF */
+int ffv1o_quant_bits(int bits, int i) {
+    const Quant q = oracle_quant(bits);
+    return quant_q(&q, i);
+}
+int ffv1o_quant(int i /* 0..255 */) { return ffv1o_quant_bits(8, i); }
 
 /* write_quant_table: run lengths of equal values over i = 0..127 */
-static void write_quant_table(RC *c, int scale_is_zero) {
+static void write_quant_table(RC *c, int scale_is_zero, const Quant *q) {
     uint8_t st[CTX_SIZE];
     int last = 0, i;
     memset(st, 128, sizeof(st));
     for (i = 1; i < 128; i++)
-        if (!scale_is_zero && ffv1o_quant(i) != ffv1o_quant(i - 1)) {
+        if (!scale_is_zero && quant_q(q, i) != quant_q(q, i - 1)) {
             put_symbol(c, st, i - last - 1, 0);
             last = i;
         }
@@ -286,7 +305,8 @@ int64_t ffv1o_extradata(int bits, int hsub, int vsub, int nh, int nv, uint8_t *o
     put_symbol(&c, st, nh - 1, 0);
     put_symbol(&c, st, nv - 1, 0);
     put_symbol(&c, st, 1, 0);      /* quant_table_set_count */
-    for (i = 0; i < 5; i++) write_quant_table(&c, i >= 3);
+    const Quant q = oracle_quant(bits);
+    for (i = 0; i < 5; i++) write_quant_table(&c, i >= 3, &q);
     put_rac(&c, st, 0);            /* states_coded[0] */
     put_symbol(&c, st, 1, 0);      /* ec: slice CRCs */
     put_symbol(&c, st, 1, 0);      /* intra: every frame a keyframe */
@@ -337,12 +357,14 @@ static inline int fold(int diff, int bits) {
 }
 
 static void encode_plane(RC *c, uint8_t (*st)[CTX_SIZE], const Plane *p, int bits) {
+    const Quant q = oracle_quant(bits);
+    const int lv = levels(&q);
     for (int y = 0; y < p->h; y++)
         for (int x = 0; x < p->w; x++) {
             int L, TL, T, TR;
             neighbours(p, x, y, &L, &TL, &T, &TR);
-            int ctx = ffv1o_quant((L - TL) & 0xFF) + 11 * ffv1o_quant((TL - T) & 0xFF) +
-                      121 * ffv1o_quant((T - TR) & 0xFF);
+            int ctx = quant_q(&q, (L - TL) & 0xFF) + lv * (quant_q(&q, (TL - T) & 0xFF) +
+                      lv * quant_q(&q, (T - TR) & 0xFF));
             int diff = px(p, x, y) - median3(L, L + T - TL, T);
             if (ctx < 0) { ctx = -ctx; diff = -diff; }
             put_symbol(c, st[ctx], fold(diff, bits), 1);

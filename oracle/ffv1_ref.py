@@ -113,7 +113,17 @@ QUANT5 = _runs([1, 4])
 QUANT9_10 = _runs([2, 6, 16, 48])
 QUANT5_10 = _runs([3, 64])
 ZERO = np.zeros(128, np.uint8)
-PIXPATH3 = _runs([1, 2, 4, 8, 16])  # pixpath's own 3-input quantiser (min(5, bit length))
+PIXPATH3 = _runs([1, 2, 4, 8, 16])  # round 4's pixpath quantiser (min(5, bit length), 666 contexts)
+
+
+def pixpath_quant(bits):
+    """The 3-input quantiser pixpath's encoder writes at a bit depth
+    (ffv1host.cpp ffv1_default_quant, ffv1_oracle.c oracle_quant)."""
+    return _runs([4, 32]) if bits > 8 else _runs([1, 3, 8])
+
+
+def pixpath_contexts(bits):
+    return 63 if bits > 8 else 172
 
 
 def ffmpeg_context1_sets(bits):

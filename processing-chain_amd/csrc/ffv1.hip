@@ -3,8 +3,9 @@
 // `-c:v ffv1 -threads 4 -level 3 -coder 1 -context 1 -slicecrc 1`
 // (lib/ffmpeg.py:993, :1047).  Bitstream per RFC 9043 / FFmpeg 7.0 ffv1enc.c;
 // the encoder's choices (range coder with the default state table, a 3-input
-// 666-context quantisation set, every frame a keyframe, caller-chosen slice
-// grid, slice CRCs) are listed in oracle/ffv1_oracle.c and DESIGN.md.
+// threshold quantisation set per bit depth -- ffv1_default_quant: 63 contexts
+// at 10 bits, 172 at 8 -- every frame a keyframe, caller-chosen slice grid,
+// slice CRCs) are listed in oracle/ffv1_oracle.c and DESIGN.md.
 //
 // GPU shape: the range coder of a slice is one serial dependency chain (each
 // binary decision updates `low/range` and an adaptive state byte), so the
@@ -46,7 +47,6 @@
 namespace pp {
 
 constexpr int kCtxSize = kFfv1CtxBytes;  // state bytes per context
-constexpr int kStateBytes = 2 * kFfv1Ctx * kCtxSize;  // luma and chroma context sets of one slice
 
 // ---- device ---------------------------------------------------------------
 struct Ffv1Args {
@@ -54,7 +54,9 @@ struct Ffv1Args {
     int64_t ls[3], fs[3];
     int w, h, bytes, bits, hsub, vsub, nh, nv, nslices;  // nslices = frames * nh * nv
     int64_t cap;            // per-slice output bytes (the 24-bit footer field bounds it)
-    uint8_t *states;        // [nslices][kStateBytes], primed to 128
+    uint8_t *states;        // [nslices / 64][hot, cold][2 * nctx][64][16], primed to 128
+    int64_t state_bytes;    // 2 * nctx * 32: one slice's luma and chroma context sets
+    int nctx;               // contexts of the record's set (Ffv1Quant::contexts)
     int64_t *sizes;         // [nslices] coded bytes, -1 = overflow
     uint32_t *crcs;         // [nslices] CRC-32 of the coded bytes
     const uint8_t *tables;  // zero[256], one[256], crc table (1 KB)
@@ -68,11 +70,14 @@ struct Ffv1Args {
     int rlpw;               // the same for ffv1_resolve_kernel
     int debug;              // PIXPATH_FFV1_DEBUG (timing ablation only; the output is wrong):
                             // 1 no block loads, 2 no block stores, 4 no record flush
+    int qthr[5];            // the record's quantiser (Ffv1Quant): thresholds, unused ones 1024
+    int qL;                 // its levels: context = q(L - TL) + qL q(TL - T) + qL^2 q(T - TR)
 };
 
-__device__ inline int dquant(int d) {  // d already & 0xFF
+// ffv1_quant (ffv1host.cpp) on the device: the number of thresholds <= |d|
+__device__ inline int dquant(int d, const int (&thr)[5]) {  // d already & 0xFF
     const int m = d < 128 ? d : (d == 128 ? 127 : 256 - d);
-    const int q = min(32 - __clz(m), 5);
+    const int q = (m >= thr[0]) + (m >= thr[1]) + (m >= thr[2]) + (m >= thr[3]) + (m >= thr[4]);
     return d < 128 ? q : -q;
 }
 
@@ -180,7 +185,7 @@ __device__ __host__ inline SliceGeo slice_geo(int g, int w, int h, int nh, int n
 // wave store one token column as one contiguous 256-B line
 // ([wave group][sample][lane], the coder's layout).  Lanes of one workgroup
 // can be in different planes (slices of unequal height), so every row pointer
-// and width is per lane.  key = plane set * 666 + |context|; the residual is
+// and width is per lane.  key = plane set * nctx + |context|; the residual is
 // negated with the context (encode_line), folded to the bit depth, int16.
 constexpr int kMX = 64;          // columns per staged chunk
 constexpr int kMS = kMX + 2;     // staged samples per row: x0 - 1 .. x0 + 64
@@ -222,7 +227,7 @@ __global__ __launch_bounds__(256) void ffv1_model_kernel(const Ffv1Args a) {
         // TL at column 0 = first sample two rows up, TR past the last column = T
         s_info[t][2] = on && y > 1 ? reinterpret_cast<const ST *>(rowb - 2 * ls)[0] : 0;
         s_info[t][3] = off + y * pw;
-        s_info[t][4] = p ? kFfv1Ctx : 0;
+        s_info[t][4] = p ? a.nctx : 0;
     }
     __syncthreads();
     const int lane = t & 63, ph = t >> 6;
@@ -258,7 +263,7 @@ __global__ __launch_bounds__(256) void ffv1_model_kernel(const Ffv1Args a) {
             const int L = x ? my[kMS + c - 1] : T;
             const int TL = x ? my[c - 1] : TL0;
             const int TR = x + 1 < pw ? my[c + 1] : T;
-            int ctx = dquant((L - TL) & 0xFF) + 11 * dquant((TL - T) & 0xFF) + 121 * dquant((T - TR) & 0xFF);
+            int ctx = dquant((L - TL) & 0xFF, a.qthr) + a.qL * (dquant((TL - T) & 0xFF, a.qthr) + a.qL * dquant((T - TR) & 0xFF, a.qthr));
             int diff = v - median3(L, L + T - TL, T);
             if (ctx < 0) {
                 ctx = -ctx;
@@ -523,8 +528,8 @@ __global__ __launch_bounds__(64) void ffv1_code_kernel(const Ffv1Args a) {
     // then cold halves: context k of slice g at [g / 64][half][k][g % 64][16]
     // -- a 128-B line holds one context's half of 8 slices (a context that is
     // hot in one slice is hot in its neighbours)
-    uint8_t *const st0 = a.states + (int64_t)(g >> 6) * (64 * kStateBytes) + (g & 63) * 16;
-    uint8_t *const co0 = st0 + 64 * kStateBytes / 2;
+    uint8_t *const st0 = a.states + (int64_t)(g >> 6) * (64 * a.state_bytes) + (g & 63) * 16;
+    uint8_t *const co0 = st0 + 64 * a.state_bytes / 2;
     constexpr int kCtxStride = 64 * 16;
     // tokens of slice g: group g / 64 of the modelling layout, lane g % 64
     const uint32_t *tp = a.tok + (int64_t)(g >> 6) * a.tok_len * 64 + (g & 63);
@@ -773,6 +778,8 @@ struct pp_ffv1_enc {
     uint8_t *pk = nullptr;     // frame packets of the last encode, back to back
     int64_t pk_cap = 0, pk_len = 0;
     int launches = 0;          // launches of the last encode (> 1: a batch was split)
+    Ffv1Quant quant;           // the record's 3-input quantiser
+    int64_t state_bytes() const { return (int64_t)2 * quant.contexts() * kCtxSize; }
     std::vector<uint8_t> extradata;
 };
 
@@ -816,8 +823,22 @@ extern "C" int pp_ffv1_encoder_create(pp_ctx *ctx, int fmt, int w, int h, int sl
     std::unique_ptr<pp_ffv1_enc> E(new pp_ffv1_enc());
     E->ctx = ctx; E->fmt = fmt; E->w = w; E->h = h; E->nh = slices_h; E->nv = slices_v; E->fi = fi;
     E->max_frames = max_frames;
+    E->quant = ffv1_default_quant(fi.depth);
     // configuration record (RFC 9043 4.2, ffv1enc.c write_extradata; ffv1host.cpp)
-    E->extradata = ffv1_write_record(fi.depth, fi.hsub, fi.vsub, slices_h, slices_v);
+    if (const char *e = PP_KNOB("PIXPATH_FFV1_QBOUNDS")) {  // measurement build: the quantiser's thresholds
+        Ffv1Quant q;
+        q.n = 0;
+        for (const char *c = e; *c && q.n < 5;) {
+            const int v = std::atoi(c);
+            if (v < 1 || v > 127 || (q.n && v <= q.thr[q.n - 1])) PP_FAIL(PP_ERR_INVALID, "PIXPATH_FFV1_QBOUNDS %s", e);
+            q.thr[q.n++] = v;
+            while (*c && *c != ',') ++c;
+            if (*c == ',') ++c;
+        }
+        if (!q.n) PP_FAIL(PP_ERR_INVALID, "PIXPATH_FFV1_QBOUNDS %s", e);
+        E->quant = q;
+    }
+    E->extradata = ffv1_write_record(fi.depth, fi.hsub, fi.vsub, slices_h, slices_v, E->quant);
     if (!ctx) {  // host-only: configuration record only
         *out = E.release();
         return PP_OK;
@@ -844,7 +865,7 @@ extern "C" int pp_ffv1_encoder_create(pp_ctx *ctx, int fmt, int w, int h, int sl
     // every slice of one frame at the worst case always fits (the last split)
     E->budget = std::max<int64_t>(ns * (E->full_raw / kBudgetDiv), (int64_t)per * E->full_raw);
     PP_HIP(hipSetDevice(ctx->device));
-    PP_HIP(hipMalloc(&E->states, (size_t)kStateBytes * ns64));
+    PP_HIP(hipMalloc(&E->states, (size_t)E->state_bytes() * ns64));
     PP_HIP(hipMalloc(&E->sizes, sizeof(int64_t) * ns));
     PP_HIP(hipMalloc(&E->off, sizeof(int64_t) * ns));
     PP_HIP(hipMalloc(&E->crcs, sizeof(uint32_t) * ns));
@@ -879,7 +900,7 @@ extern "C" int pp_ffv1_extradata(const pp_ffv1_enc *E, uint8_t *out, int cap) {
 extern "C" int pp_ffv1_encoder_memory(const pp_ffv1_enc *E, int64_t *bytes) {
     if (!E || !bytes) PP_FAIL(PP_ERR_INVALID, "null argument");
     const int64_t ns = (int64_t)E->nh * E->nv * E->max_frames, ns64 = (ns + 63) / 64 * 64;
-    *bytes = E->ctx ? (int64_t)kStateBytes * ns64 + (8 + 8 + 4 + 4) * ns + 4 * ns64 * E->tok_len + 4 * E->budget +
+    *bytes = E->ctx ? E->state_bytes() * ns64 + (8 + 8 + 4 + 4) * ns + 4 * ns64 * E->tok_len + 4 * E->budget +
                           1536 + E->pk_cap
                     : 0;
     return PP_OK;
@@ -935,8 +956,12 @@ extern "C" int64_t pp_ffv1_encode_packets(pp_ffv1_enc *E, const pp_frames *src, 
         a.cap = E->cap; a.states = E->states; a.sizes = E->sizes; a.crcs = E->crcs;
         a.tables = E->tables;
         a.tok = E->tok; a.tok_len = E->tok_len; a.raw = E->raw; a.raw_cap = rcap; a.nraw = E->nraw;
+        for (int k = 0; k < 5; ++k) a.qthr[k] = k < E->quant.n ? E->quant.thr[k] : 1024;
+        a.qL = E->quant.levels();
+        a.nctx = E->quant.contexts();
+        a.state_bytes = E->state_bytes();
         const int nwg = (ns + 63) / 64;
-        PP_HIP(hipMemsetAsync(E->states, 128, (size_t)kStateBytes * nwg * 64, st));  // every context of every slice: 128
+        PP_HIP(hipMemsetAsync(E->states, 128, (size_t)E->state_bytes() * nwg * 64, st));  // every context of every slice: 128
         if (a.bytes == 2)
             hipLaunchKernelGGL(ffv1_model_kernel<uint16_t>, dim3((unsigned)E->rows_max, nwg), dim3(256), 0, st, a);
         else

@@ -58,6 +58,7 @@ struct Ffv1DecArgs {
     const uint8_t *tables;       // zero[256], one[256] (the record's), crc table, x^(8 * 2^j)
     const int16_t *quant;        // [ntables][5][256] (scaled)
     const uint4 *init;           // [contexts][hot 16 | cold 16] initial states, split as the state halves
+    int qthr[5];                 // PIX: the first quantiser's thresholds (Ffv1Quant), unused ones 1024
 };
 
 // The slice's range decoder (rangecoder.h get_rac / refill) on register-held
@@ -279,12 +280,12 @@ __device__ __forceinline__ void dblk_store(uint8_t *p, const uint32_t (&b)[8]) {
 
 __device__ __forceinline__ int dmedian3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 
-// pixpath's own first quantiser (ffv1host.cpp ffv1_quant: min(5, bit length
-// |d|), odd-mirrored, scale 1) as ALU code: the only lookup that depends on
-// the sample just decoded leaves LDS
-__device__ __forceinline__ int dquant0(int d) {  // d already & 0xFF
+// A pixpath-form first quantiser (ffv1host.cpp ffv1_quant: the number of
+// thresholds <= |d|, odd-mirrored, scale 1) as ALU code: the only lookup that
+// depends on the sample just decoded leaves LDS
+__device__ __forceinline__ int dquant0(int d, const int (&thr)[5]) {  // d already & 0xFF
     const int m = d < 128 ? d : (d == 128 ? 127 : 256 - d);
-    const int q = min(32 - __clz(m), 5);
+    const int q = (m >= thr[0]) + (m >= thr[1]) + (m >= thr[2]) + (m >= thr[3]) + (m >= thr[4]);
     return d < 128 ? q : -q;
 }
 
@@ -479,7 +480,7 @@ __global__ __launch_bounds__(64) void ffv1_decode_kernel(const Ffv1DecArgs a) {
                     if constexpr (!PIX) nTT = (y > 1 && x + 1 < pw) ? two[x + 1] : 0;
                     int ctx;
                     if constexpr (PIX)
-                        ctx = dquant0((L - TL) & 0xFF) + q[256 + ((TL - T) & 0xFF)] + q[512 + ((T - TR) & 0xFF)];
+                        ctx = dquant0((L - TL) & 0xFF, a.qthr) + q[256 + ((TL - T) & 0xFF)] + q[512 + ((T - TR) & 0xFF)];
                     else
                         ctx = q[(L - TL) & 0xFF] + q[256 + ((TL - T) & 0xFF)] + q[512 + ((T - TR) & 0xFF)] +
                               q[768 + ((LL - L) & 0xFF)] + q[1024 + ((TT - T) & 0xFF)];
@@ -543,6 +544,7 @@ struct pp_ffv1_dec {
     int w = 0, h = 0, max_frames = 0;
     Ffv1Record rec;
     bool pix = false;  // pixpath's own 3-input set (ALU first quantiser, one line row)
+    Ffv1Quant pq;      // its thresholds
     uint8_t *pkt = nullptr, *states = nullptr, *tables = nullptr, *carry = nullptr;
     int64_t pkt_cap = 0, *soff = nullptr, *slen = nullptr;
     int *gop = nullptr;
@@ -577,12 +579,26 @@ void split_states(const uint8_t *st, uint8_t hot[16], uint8_t cold[16]) {
     for (int i = 0; i < 4; ++i) hot[11 + i] = st[22 + i];
 }
 
-bool pixpath_tables(const Ffv1Record &r) {
+// A record of pixpath's form: one set of 3 inputs whose quantisers are one
+// threshold quantiser (Ffv1Quant, up to 5 thresholds) at scales 1, L, L^2 --
+// what pixpath's encoder writes, whichever thresholds it chose.  *q gets the
+// thresholds (the kernel's ALU first quantiser).
+bool pixpath_tables(const Ffv1Record &r, Ffv1Quant *q) {
     if (r.ntables != 1) return false;
+    Ffv1Quant t;
+    t.n = 0;
+    for (int i = 1; i < 128; ++i) {
+        const int d = r.quant[0][0][i] - r.quant[0][0][i - 1];
+        if (d < 0 || d > 1 || (d == 1 && t.n == 5)) return false;
+        if (d == 1) t.thr[t.n++] = i;
+    }
+    if (r.quant[0][0][0] != 0) return false;
+    const int L = t.levels();
     for (int i = 0; i < 256; ++i)
-        if (r.quant[0][0][i] != ffv1_quant(i) || r.quant[0][1][i] != 11 * ffv1_quant(i) ||
-            r.quant[0][2][i] != 121 * ffv1_quant(i) || r.quant[0][3][i] || r.quant[0][4][i])
+        if (r.quant[0][0][i] != ffv1_quant(i, t) || r.quant[0][1][i] != L * ffv1_quant(i, t) ||
+            r.quant[0][2][i] != L * L * ffv1_quant(i, t) || r.quant[0][3][i] || r.quant[0][4][i])
             return false;
+    *q = t;
     return true;
 }
 
@@ -600,7 +616,7 @@ extern "C" int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extra, int ext
     if (R.bits != 8 && R.bits != 10) PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 decoder: %d-bit samples (8 or 10)", R.bits);
     if (R.hsub == 0 && R.vsub == 1) PP_FAIL(PP_ERR_UNSUPPORTED, "FFV1 decoder: 4:4:0 chroma");
     D->ctx = ctx; D->w = w; D->h = h; D->max_frames = max_frames;
-    D->pix = pixpath_tables(R);
+    D->pix = pixpath_tables(R, &D->pq);
     int wmax = 0;
     for (int i = 0; i < R.nh; ++i)
         wmax = std::max(wmax, (int)((int64_t)(i + 1) * w / R.nh - (int64_t)i * w / R.nh));
@@ -785,6 +801,7 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     }
     a.state_bytes = sb;
     a.states = D->states; a.cold = D->states + half; a.status = D->status; a.tables = D->tables; a.quant = D->dquant;
+    for (int k = 0; k < 5; ++k) a.qthr[k] = k < D->pq.n ? D->pq.thr[k] : 1024;
     a.init = D->dinit;
     // chains per workgroup: the LDS bound, spread over the CUs when chains are few (long GOPs)
     a.lpw = std::max(1, std::min(D->lpw, (nchains + D->ctx->cus - 1) / std::max(1, D->ctx->cus)));

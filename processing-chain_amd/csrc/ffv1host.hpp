@@ -12,7 +12,6 @@
 
 namespace pp {
 
-constexpr int kFfv1Ctx = 666;   // (11^3 + 1) / 2 contexts of the 3-input set the encoder writes
 constexpr int kFfv1CtxBytes = 32;  // state bytes per context
 constexpr int kFfv1MaxCtx = 16384; // (32768 + 1) / 2: read_quant_tables' bound on one set
 constexpr int kFfv1MaxTables = 8;  // MAX_QUANT_TABLES
@@ -21,13 +20,27 @@ constexpr int kFfv1MaxTables = 8;  // MAX_QUANT_TABLES
 void rac_states(uint8_t zero[256], uint8_t one[256]);
 // AV_CRC_32_IEEE: polynomial 0x04C11DB7, MSB first, initial 0, no final xor
 void crc_table(uint32_t t[256]);
-// the 3-input quantiser the encoder's record describes: min(5, bit length |d|), odd-mirrored
-int ffv1_quant(int i);
+// A 3-input threshold quantiser: the level of |d| (d = 0..127) is the number
+// of thresholds <= |d|, odd-mirrored for d = 128..255 (read_quant_table's
+// shape; every FFV1 input quantiser has it).  Ffv1Quant() is thresholds 1, 2,
+// 4, 8, 16 = min(5, bit length |d|): 11 levels, (11^3 + 1) / 2 = 666 contexts
+// (pixpath's encoder up to round 5); the encoder now writes ffv1_default_quant.
+struct Ffv1Quant {
+    int n = 5;
+    int thr[5] = {1, 2, 4, 8, 16};
+    int levels() const { return 2 * n + 1; }
+    int contexts() const { return (levels() * levels() * levels() + 1) / 2; }
+};
+int ffv1_quant(int i, const Ffv1Quant &q);
+// The quantiser pixpath's encoder writes for a bit depth (oracle/ffv1_oracle.c
+// oracle_quant restates the same rule).
+Ffv1Quant ffv1_default_quant(int depth);
 
 // The configuration record (RFC 9043 4.2, ffv1enc.c write_extradata) of
 // pixpath's encoder: version 3, range coder with the default table, one
-// 3-input quantisation set, slice CRCs, intra; CRC-32 parity appended.
-std::vector<uint8_t> ffv1_write_record(int depth, int hsub, int vsub, int slices_h, int slices_v);
+// 3-input quantisation set (q), slice CRCs, intra; CRC-32 parity appended.
+std::vector<uint8_t> ffv1_write_record(int depth, int hsub, int vsub, int slices_h, int slices_v,
+                                       const Ffv1Quant &q);
 
 // What the decoder needs from a configuration record (RFC 9043 4.2,
 // ffv1dec.c read_extra_header): version 3, range coder with the default

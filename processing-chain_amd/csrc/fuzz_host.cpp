@@ -98,14 +98,14 @@ long fuzz_records(Rng &r, int iters) {
         const int *f = fmts[r.below(4)];
         const int nh = 1 + r.below(16), nv = 1 + r.below(16);
         const int w = 64 * (1 + r.below(30)), h = 64 * (1 + r.below(17));
-        std::vector<uint8_t> rec = ffv1_write_record(f[0], f[1], f[2], nh, nv);
+        std::vector<uint8_t> rec = ffv1_write_record(f[0], f[1], f[2], nh, nv, ffv1_default_quant(f[0]));
         pp::Ffv1Record out;
         std::string err;
         if (it % 8 == 0) {  // the valid record round trips
             std::vector<uint8_t> b = exact(rec);
             const int rc = ffv1_parse_record(b.data(), (int)b.size(), w, h, &out, &err);
             CHECK(rc == 0 && out.bits == f[0] && out.hsub == f[1] && out.vsub == f[2] && out.nh == nh &&
-                      out.nv == nv && out.ec == 1 && out.ntables == 1 && out.ctx_count[0] == kFfv1Ctx && out.intra == 1 &&
+                      out.nv == nv && out.ec == 1 && out.ntables == 1 && out.ctx_count[0] == ffv1_default_quant(f[0]).contexts() && out.intra == 1 &&
                       out.coder == 1,
                   "record %d/%d/%d %dx%d did not round trip: %d %s", f[0], f[1], f[2], nh, nv, rc, err.c_str());
         }

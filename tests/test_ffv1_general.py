@@ -48,7 +48,8 @@ def test_pixpath_profile_equals_the_intra_restatement(name, fid, bits, hs, vs, g
     with the intra path's neighbour rules."""
     rng = np.random.default_rng(bits * 7 + grid[0])
     w, h = 330, 190
-    pf = ref.make_prof(bits, hs, vs, *grid, [[ref.PIXPATH3] * 3 + [ref.ZERO] * 2], tidx=(0, 0), coder=1, gop=1)
+    q = ref.pixpath_quant(bits)
+    pf = ref.make_prof(bits, hs, vs, *grid, [[q] * 3 + [ref.ZERO] * 2], tidx=(0, 0), coder=1, gop=1)
     enc = ref.GenEncoder(pf, w, h)
     for f in (synth.noise_frame(rng, fid, w, h), synth.smooth_frame(2, fid, w, h)):
         assert enc.encode(f) == ref.encode_frame(f, bits, hs, vs, *grid)
@@ -151,8 +152,36 @@ def test_product_parser_reads_ffmpeg_like_records(name, fid, bits, hs, vs, init)
 def test_product_parser_marks_pixpath_records(name, fid, bits, hs, vs):
     from pixpath import ffv1
     dec = ffv1.Ffv1Decoder(ref.extradata(bits, hs, vs, 8, 8), 1920, 1080, host_only=True)
-    assert _native_info(dec) == {"micro": 4, "coder": 1, "tables": 1, "max_ctx": 666, "intra": 1, "ec": 1,
+    assert _native_info(dec) == {"micro": 4, "coder": 1, "tables": 1, "max_ctx": ref.pixpath_contexts(bits),
+                                 "intra": 1, "ec": 1,
                                  "init_mask": 0, "pix": 1}
+
+
+@pytest.mark.parametrize("bounds", [[1, 2, 4, 8, 16], [3, 8, 32], [2, 6, 16, 48], [4, 32], [1, 3, 8]])
+def test_product_parser_marks_threshold_quantisers(bounds):
+    """Any one-set, 3-input record whose quantisers are one threshold
+    quantiser at scales 1, L, L^2 takes the decoder's pixpath path (ALU first
+    quantiser, one line row): the thresholds are read back from the record."""
+    from pixpath import ffv1
+    t = ref._runs(bounds)
+    pf = ref.make_prof(10, 1, 0, 8, 8, [[t, t, t, ref.ZERO, ref.ZERO]], tidx=(0, 0), coder=1, gop=1)
+    dec = ffv1.Ffv1Decoder(ref.gen_extradata(pf), 1920, 1080, host_only=True)
+    L = 2 * len(bounds) + 1
+    info = _native_info(dec)
+    assert info["pix"] == 1 and info["max_ctx"] == (L ** 3 + 1) // 2 and info["tables"] == 1
+
+
+def test_product_parser_leaves_other_quantisers_general():
+    """A set whose three inputs use different quantisers (every FFV1 input
+    quantiser is threshold-shaped: read_quant_table's runs step by one), or
+    whose inputs 4 and 5 are used, decodes through the general path."""
+    from pixpath import ffv1
+    for sets in ([[ref.QUANT11, ref.PIXPATH3, ref.PIXPATH3, ref.ZERO, ref.ZERO]],
+                 [[ref.PIXPATH3, ref.PIXPATH3, ref.QUANT5, ref.ZERO, ref.ZERO]],
+                 [[ref.PIXPATH3, ref.PIXPATH3, ref.PIXPATH3, ref.QUANT5, ref.ZERO]]):
+        pf = ref.make_prof(10, 1, 0, 8, 8, sets, tidx=(0, 0), coder=1, gop=1)
+        dec = ffv1.Ffv1Decoder(ref.gen_extradata(pf), 1920, 1080, host_only=True)
+        assert _native_info(dec)["pix"] == 0
 
 
 def test_product_parser_refuses_corrupt_records():

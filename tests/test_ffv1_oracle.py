@@ -61,7 +61,7 @@ def test_product_configuration_record(name, fid, bits, hs, vs, grid):
     assert rc == 0 and info["crc_ok"] == 1
     assert (info["version"], info["micro_version"], info["coder_type"], info["ec"], info["intra"]) == (3, 4, 1, 1, 1)
     assert (info["bits"], info["hsub"], info["vsub"]) == (bits, hs, vs)
-    assert (info["num_h_slices"], info["num_v_slices"], info["context_count"]) == (grid[0], grid[1], 666)
+    assert (info["num_h_slices"], info["num_v_slices"], info["context_count"]) == (grid[0], grid[1], ref.pixpath_contexts(bits))
     assert ref.crc(x) == 0
 
 
