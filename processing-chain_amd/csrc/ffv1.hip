@@ -195,8 +195,10 @@ __global__ __launch_bounds__(256) void ffv1_model_kernel(const Ffv1Args a) {
     __shared__ int s_row[64 * kMLane];        // [lane][top, cur][column x0 - 1 + j]
     __shared__ uint64_t s_ptr[64][2];         // [lane][row above, row]
     __shared__ int s_info[64][5];             // pw, has-T, TL0, token offset, context key base
+    __shared__ int s_q[256];                  // quantiser level of d & 0xFF (ffv1_quant)
     const int t = threadIdx.x;
     const int wg = blockIdx.y;
+    s_q[t] = dquant(t, a.qthr);
     if (t < 64) {
         const int g = wg * 64 + t;
         const bool live = g < a.nslices;
@@ -241,18 +243,35 @@ __global__ __launch_bounds__(256) void ffv1_model_kernel(const Ffv1Args a) {
     for (int x0 = 0; x0 < pw_max; x0 += kMX) {
         if (x0) __syncthreads();  // the previous chunk's LDS reads are done
         // stage columns x0 - 1 .. x0 + 64 of the row above and the row of every
-        // lane: thread t takes half t & 1 of segment t >> 1 (lane j, row rw),
-        // so its row pointer and bounds are fixed for the chunk (no per-sample
-        // divisions or LDS lookups); successive samples of a thread hit L1
+        // lane (segment = lane j, row rw) as 16-byte pieces of the aligned span
+        // x0 - 8 .. x0 + 72: thread t takes pieces t, t + 256, ... of the
+        // chunk, so consecutive threads read consecutive bytes of one slice row
+        // (a per-thread walk of 2-byte loads, one row per lane, was bound by
+        // the L1 -> L2 requests: 3.3e9 per 600 frames, profiles/r5/ffv1_pmc.txt).
+        // A piece past the row's ends, or of a row not 16-byte aligned, is read
+        // sample by sample with the bounds check (zeros outside the row).
         {
-            const int seg = t >> 1, j = seg >> 1, rw = seg & 1, c0 = (t & 1) * (kMS / 2);
-            const ST *rp = reinterpret_cast<const ST *>(s_ptr[j][rw]);
-            const int lim = (rw || s_info[j][1]) ? s_info[j][0] : 0;  // row above absent: zeros
-            int *dst = s_row + j * kMLane + rw * kMS;
-#pragma unroll 11
-            for (int col = c0; col < c0 + kMS / 2; ++col) {
-                const int x = x0 - 1 + col;
-                dst[col] = (x >= 0 && x < lim) ? (int)rp[x] : 0;
+            constexpr int SP = 16 / (int)sizeof(ST);  // samples per piece
+            constexpr int NP = (kMX + 16) / SP;       // pieces per segment
+            for (int i = t; i < 128 * NP; i += 256) {
+                const int seg = i / NP, pc = i - seg * NP, j = seg >> 1, rw = seg & 1;
+                const ST *rp = reinterpret_cast<const ST *>(s_ptr[j][rw]);
+                const int lim = (rw || s_info[j][1]) ? s_info[j][0] : 0;  // row above absent: zeros
+                const int s0 = x0 - 8 + pc * SP;
+                int *dst = s_row + j * kMLane + rw * kMS + (s0 - (x0 - 1));  // column of sample s0
+                ST v[SP];
+                if (s0 >= 0 && s0 + SP <= lim && (reinterpret_cast<uintptr_t>(rp) & 15) == 0) {
+                    const uint4 q = *reinterpret_cast<const uint4 *>(rp + s0);
+                    __builtin_memcpy(v, &q, 16);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < SP; ++e) v[e] = (s0 + e >= 0 && s0 + e < lim) ? rp[s0 + e] : (ST)0;
+                }
+#pragma unroll
+                for (int e = 0; e < SP; ++e) {
+                    const int col = s0 - (x0 - 1) + e;
+                    if (col >= 0 && col < kMS) dst[e] = (int)v[e];
+                }
             }
         }
         __syncthreads();
@@ -263,7 +282,7 @@ __global__ __launch_bounds__(256) void ffv1_model_kernel(const Ffv1Args a) {
             const int L = x ? my[kMS + c - 1] : T;
             const int TL = x ? my[c - 1] : TL0;
             const int TR = x + 1 < pw ? my[c + 1] : T;
-            int ctx = dquant((L - TL) & 0xFF, a.qthr) + a.qL * (dquant((TL - T) & 0xFF, a.qthr) + a.qL * dquant((T - TR) & 0xFF, a.qthr));
+            int ctx = s_q[(L - TL) & 0xFF] + a.qL * (s_q[(TL - T) & 0xFF] + a.qL * s_q[(T - TR) & 0xFF]);
             int diff = v - median3(L, L + T - TL, T);
             if (ctx < 0) {
                 ctx = -ctx;
