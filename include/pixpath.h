@@ -249,7 +249,8 @@ int64_t pp_ivf_frame_sizes(const uint8_t *buf, int64_t n, int64_t *sizes, int64_
 /* ---- FFV1 AVPVS encoder -----------------------
  * Replaces the `-c:v ffv1 -level 3 -coder 1 -context 1 -slicecrc 1` encode of
  * the AVPVS (lib/ffmpeg.py:993, :1047): FFV1 version 3 (RFC 9043), range
- * coder, slice CRCs, every frame a keyframe, slices_h x slices_v slices per
+ * coder, slice CRCs, every frame a keyframe, one 3-input quantisation set
+ * (63 contexts at 10 bits, 172 at 8), slices_h x slices_v slices per
  * frame (<= 256), one GPU lane per slice.  Bitstream choices and the parity
  * status (unpinned: no FFV1 decoder exists here) are in DESIGN.md.
  * pp_ffv1_encoder_create with ctx == NULL builds the configuration record only.
@@ -307,8 +308,10 @@ int pp_ffv1_decode(pp_ffv1_dec *dec, const uint8_t *packets, const int64_t *fram
                    const pp_frames *dst, void *stream);
 /* ABI v6.  The record as parsed: up to n of micro_version, coder_type,
  * quantisation table sets, largest context count, intra, ec, bit mask of the
- * sets with transmitted initial states, 1 if the tables are pixpath's own
- * 3-input set; returns the count written. */
+ * sets with transmitted initial states, 1 if the tables are of pixpath's
+ * form (one 3-input set: one threshold quantiser at scales 1, L, L^2 -- what
+ * pp_ffv1_encode writes: 63 contexts at 10 bits, 172 at 8; round-4 files: 666),
+ * decoded by the one-line-row path; returns the count written. */
 int pp_ffv1_decoder_info(const pp_ffv1_dec *dec, int *info, int n);
 int pp_ffv1_decoder_reset(pp_ffv1_dec *dec);
 int pp_ffv1_decoder_geometry(const pp_ffv1_dec *dec, int *slices_per_workgroup, int *row_cap);
