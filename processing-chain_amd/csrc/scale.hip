@@ -1112,7 +1112,8 @@ extern "C" int pp_scale_chain_plan_create(pp_ctx *ctx, int src_fmt, int sw, int 
     pp_scale_plan *lp = nullptr;
     // PIXPATH_CHAIN_ONE_LAUNCH (measurement build): keep luma in the chroma launch
     if (v422 && !PP_KNOB("PIXPATH_CHAIN_ONE_LAUNCH") &&
-        plan_create(ctx, src_fmt, sw, sh, PP_FMT_YUV420P, dw, dh, flags, p0, p1, false, &lp, 0, false) == PP_OK) {
+        plan_create(ctx, src_fmt, sw, sh, PP_FMT_YUV420P, dw, dh, flags, p0, p1, false, &lp,
+                    PP_KNOB("PIXPATH_CHAIN_LUMA_CHO") ? std::atoi(PP_KNOB("PIXPATH_CHAIN_LUMA_CHO")) : 0, false) == PP_OK) {
         if (lp->kind == pp_scale_plan::GENERIC && lp->fast_hw > 0 && lp->fast_tw == 256) {
             P->luma = lp;
             lp->fjob[0].fuse = P->chain_out > 8 ? 1 : 0;
@@ -1309,7 +1310,8 @@ int launch_packed(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, 
 // planes `pl` (job, source / destination plane index), tile bases renumbered
 // for the launch
 int launch_chain_planes(pp_scale_plan *P, const pp::PlaneJob *const *jobs, const int *pl, int np, int hw, size_t lds,
-                        const pp_frames *src, const pp_frames *dst, int nframes, hipStream_t st) {
+                        const pp_frames *src, const pp_frames *dst, int nframes, hipStream_t st,
+                        bool luma_only = false) {
     using namespace pp;
     ScaleArgs a{};
     a.nplanes = np;
@@ -1335,7 +1337,12 @@ int launch_chain_planes(pp_scale_plan *P, const pp::PlaneJob *const *jobs, const
     for (int i = 0; i < np; ++i)
         a.vec_dst &= aligned(a.dst[i], a.dls[i], nframes > 1 ? a.dfs[i] : 0, P->chain_out == 8 ? 4 : 8);
     const int vtm = strip_vtm_bucket(vtp);
-    KernelFn k = P->si.depth == 8 ? pick_strip_chain_u8(P->chain_out, hw, vtm) : pick_strip_chain_u16(P->chain_out, hw, vtm);
+    // the luma launch of a 10-bit chain (fuse 1 into 10 bits) takes its own
+    // instance without the ring2 / second-stage code (FUSE 9)
+    const bool l9 = luma_only && P->chain_out == 10 && jobs[0]->fuse == 1 && !PP_KNOB("PIXPATH_CHAIN_NO_LUMA9");
+    KernelFn k = l9 ? (P->si.depth == 8 ? pick_strip_luma_u8(hw, vtm) : pick_strip_luma_u16(hw, vtm))
+                    : P->si.depth == 8 ? pick_strip_chain_u8(P->chain_out, hw, vtm)
+                                       : pick_strip_chain_u16(P->chain_out, hw, vtm);
     if (!k) PP_FAIL(PP_ERR_UNSUPPORTED, "no chain kernel for window %d", hw);
     a.tiles = tiles;
     const int fmax = std::max(1, (1 << 30) / tiles);
@@ -1382,7 +1389,7 @@ int launch_chain(pp_scale_plan *P, const pp_frames *src, const pp_frames *dst, i
         const PlaneJob *lj[1] = {&P->luma->fjob[0]};
         const int lpl[1] = {0};
         if (int rc = launch_chain_planes(P, lj, lpl, 1, P->luma->fast_hw, P->luma->fast_lds_plane[0], src, dst,
-                                         nframes, ls))
+                                         nframes, ls, true))
             return rc;
         const PlaneJob *cj[2] = {&P->fjob[1], &P->fjob[2]};
         const int cpl[2] = {1, 2};

@@ -127,6 +127,14 @@ template <int HW, int VTM>
 constexpr int strip_chain_min_waves() {
     return (HW <= 4 && VTM <= 3) ? 6 : ((HW <= 10 && VTM <= 5) || (HW == 12 && VTM <= 3)) ? 4 : 3;
 }
+#ifndef PIXPATH_LUMA9_WAVES
+#define PIXPATH_LUMA9_WAVES 6
+#endif
+// FUSE 9 (a chain's luma launch alone): its own budget where the window is narrow
+template <int HW, int VTM, int FUSE>
+constexpr int strip_fused_min_waves() {
+    return FUSE == 9 && HW <= 4 && VTM <= 3 ? PIXPATH_LUMA9_WAVES : strip_chain_min_waves<HW, VTM>();
+}
 // Instances with register room for the clamped V-pass copy (a second
 // instantiation of the row loop): the rest keep the per-lane path rather than
 // spill (tools/check_spills.sh: 8-bit sources into 8-bit rows with 4-dword
@@ -137,7 +145,7 @@ constexpr bool strip_clamp_path() {
 }
 
 template <typename ST, int OUTB, int HW, int VTM, int FUSE = 0, int TW = 256>
-__global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() : strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
+__global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUSE>() : strip_min_waves<(int)sizeof(ST), OUTB, HW, VTM>())) void strip_kernel(const ScaleArgs a) {
     static_assert(TW == 256 || TW == 512, "strip width");
     // DIRECT (8-dword windows: the 2:1 downscales of config 3): no staged
     // source rows -- a lane loads its window's 16 source samples of a row
@@ -257,7 +265,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
 
     int y_begin = seg * J.seg_h, y_end = min(J.dh, y_begin + J.seg_h);
     int r2lo = 0, r2hi = 0;  // fuse 2: the second-stage rows this segment stores
-    if constexpr (FUSE >= 8) {
+    if constexpr (FUSE >= 8 && FUSE != 9) {
         if (J.fuse == 2) {  // first-stage rows of the segment plus the halo its second-stage rows read
             const kconst int32_t *sg = as_kconst<int32_t>(J.seg2) + 4 * seg;
             y_begin = sg[0];
@@ -295,7 +303,10 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
     const int64_t dls = a.dls[p];
     const int vtp = J.vtp;
     const int jdw = J.dw;
-    const int jfuse = FUSE >= 8 ? J.fuse : 0;
+    // FUSE 9: a chain plan's luma launch alone (fuse 1 into 10 bits: no ring2,
+    // no second stage, a compile-time mode)
+    const int jfuse = FUSE == 9 ? 1 : FUSE >= 8 ? J.fuse : 0;
+    constexpr int OUT2 = FUSE == 9 ? 10 : FUSE;  // the chain's output bits
     const kconst int32_t *vrow = as_kconst<int32_t>(J.vrow16);
     for (int y0 = y_begin; y0 < y_end; y0 += cho) {
         const int ci = y0 / cho;
@@ -509,12 +520,12 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
                             continue;
                         }
                         if (jfuse == 1) {  // identity second stage: one 4096 tap on x << 7
-                            constexpr int r2 = FUSE == 8 ? 64 << 12 : 1 << (10 + 16 - FUSE);
-                            constexpr int s2 = FUSE == 8 ? 19 : 11 + 16 - FUSE;
+                            constexpr int r2 = OUT2 == 8 ? 64 << 12 : 1 << (10 + 16 - OUT2);
+                            constexpr int s2 = OUT2 == 8 ? 19 : 11 + 16 - OUT2;
                             int w[4];
 #pragma unroll
                             for (int j = 0; j < 4; ++j) w[j] = ((o[j] << 19) + r2) >> s2;
-                            store4<FUSE>(drow_p, vxo, w, CL || (lane_full && a.vec_dst), jdw);
+                            store4<OUT2>(drow_p, vxo, w, CL || (lane_full && a.vec_dst), jdw);
                             __builtin_amdgcn_sched_barrier(0);
                             continue;
                         }
@@ -551,7 +562,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_chain_min_waves<HW, VTM>() :
         } else {
             vdispatch(std::false_type{});
         }
-        if constexpr (FUSE >= 8) {
+        if constexpr (FUSE >= 8 && FUSE != 9) {
             // ---- second stage (fuse 2): vertical filter of the ring2 rows ----
             if (jfuse == 2 && !(PP_ABLATE(a.debug) & 16)) {  // debug 16: no second stage (timing only)
                 __syncthreads();  // this chunk's first-stage rows are in ring2
