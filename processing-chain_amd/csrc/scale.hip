@@ -1340,9 +1340,14 @@ int launch_chain_planes(pp_scale_plan *P, const pp::PlaneJob *const *jobs, const
     // the luma launch of a 10-bit chain (fuse 1 into 10 bits) takes its own
     // instance without the ring2 / second-stage code (FUSE 9)
     const bool l9 = luma_only && P->chain_out == 10 && jobs[0]->fuse == 1 && !PP_KNOB("PIXPATH_CHAIN_NO_LUMA9");
-    KernelFn k = l9 ? (P->si.depth == 8 ? pick_strip_luma_u8(hw, vtm) : pick_strip_luma_u16(hw, vtm))
-                    : P->si.depth == 8 ? pick_strip_chain_u8(P->chain_out, hw, vtm)
-                                       : pick_strip_chain_u16(P->chain_out, hw, vtm);
+    // ... and the chroma launch (every plane fuse 2) FUSE 11
+    bool c11 = !luma_only && P->luma && P->chain_out == 10 && !PP_KNOB("PIXPATH_CHAIN_NO_CHROMA11");
+    for (int i = 0; i < np; ++i) c11 = c11 && jobs[i]->fuse == 2;
+    const bool u8 = P->si.depth == 8;
+    KernelFn k = l9 ? (u8 ? pick_strip_luma_u8(hw, vtm) : pick_strip_luma_u16(hw, vtm))
+                    : c11 ? (u8 ? pick_strip_chroma_u8(hw, vtm) : pick_strip_chroma_u16(hw, vtm)) : nullptr;
+    if (!k)  // (FUSE 9 / 11 exist for narrow windows only)
+        k = u8 ? pick_strip_chain_u8(P->chain_out, hw, vtm) : pick_strip_chain_u16(P->chain_out, hw, vtm);
     if (!k) PP_FAIL(PP_ERR_UNSUPPORTED, "no chain kernel for window %d", hw);
     a.tiles = tiles;
     const int fmax = std::max(1, (1 << 30) / tiles);

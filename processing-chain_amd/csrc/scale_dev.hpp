@@ -222,6 +222,8 @@ KernelFn pick_strip_chain_u16(int out2, int hw, int vtm);
 KernelFn pick_strip_chain_u8(int out2, int hw, int vtm);
 KernelFn pick_strip_luma_u16(int hw, int vtm);  // FUSE 9: a chain's luma launch into 10 bits
 KernelFn pick_strip_luma_u8(int hw, int vtm);
+KernelFn pick_strip_chroma_u16(int hw, int vtm);  // FUSE 11: a chain's chroma launch into 10 bits
+KernelFn pick_strip_chroma_u8(int hw, int vtm);
 // GENERIC_UYVY plans: 8-bit samples stored straight into the packed uyvy422 row
 KernelFn pick_strip_packed_u16(int hw, int vtm);
 KernelFn pick_strip_packed_u8(int hw, int vtm);

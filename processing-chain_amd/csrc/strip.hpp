@@ -303,10 +303,11 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
     const int64_t dls = a.dls[p];
     const int vtp = J.vtp;
     const int jdw = J.dw;
-    // FUSE 9: a chain plan's luma launch alone (fuse 1 into 10 bits: no ring2,
-    // no second stage, a compile-time mode)
-    const int jfuse = FUSE == 9 ? 1 : FUSE >= 8 ? J.fuse : 0;
-    constexpr int OUT2 = FUSE == 9 ? 10 : FUSE;  // the chain's output bits
+    // FUSE 9 / 11: a 10-bit chain plan's luma launch alone (fuse 1: no ring2,
+    // no second stage) / chroma launch alone (fuse 2), the mode a compile-time
+    // constant
+    const int jfuse = FUSE == 9 ? 1 : FUSE == 11 ? 2 : FUSE >= 8 ? J.fuse : 0;
+    constexpr int OUT2 = FUSE == 9 || FUSE == 11 ? 10 : FUSE;  // the chain's output bits
     const kconst int32_t *vrow = as_kconst<int32_t>(J.vrow16);
     for (int y0 = y_begin; y0 < y_end; y0 += cho) {
         const int ci = y0 / cho;
@@ -627,13 +628,13 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
                                 int acc[4];
 #pragma unroll
                                 for (int j = 0; j < 4; ++j)
-                                    acc[j] = (acc2[h][j] << 7) + (FUSE == 8 ? 64 << 12 : 1 << (10 + 16 - FUSE));
+                                    acc[j] = (acc2[h][j] << 7) + (OUT2 == 8 ? 64 << 12 : 1 << (10 + 16 - OUT2));
                                 if ((!CL && !lane_any) || r2 >= hi2) continue;
-                                constexpr int s2 = FUSE == 8 ? 19 : 11 + 16 - FUSE;
+                                constexpr int s2 = OUT2 == 8 ? 19 : 11 + 16 - OUT2;
                                 int w[4];
 #pragma unroll
-                                for (int j = 0; j < 4; ++j) w[j] = min(max(acc[j] >> s2, 0), (1 << FUSE) - 1);
-                                store4<FUSE>(dbase + (int64_t)r2 * dls, vxo, w, CL || (lane_full && a.vec_dst), jdw);
+                                for (int j = 0; j < 4; ++j) w[j] = min(max(acc[j] >> s2, 0), (1 << OUT2) - 1);
+                                store4<OUT2>(dbase + (int64_t)r2 * dls, vxo, w, CL || (lane_full && a.vec_dst), jdw);
                             }
                             __builtin_amdgcn_sched_barrier(0);
                         }

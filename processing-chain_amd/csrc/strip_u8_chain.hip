@@ -11,11 +11,6 @@ KernelFn pick_strip_chain_u8(int out2, int hw, int vtm) {
     PP_STRIP_HW_F(uint8_t, 8, 10)
 }
 
-// a chain plan's luma launch alone into 10 bits (FUSE 9: no ring2 code)
-KernelFn pick_strip_luma_u8(int hw, int vtm) {
-    PP_STRIP_HW_F(uint8_t, 8, 9)
-}
-
 KernelFn pick_strip_packed_u8(int hw, int vtm) {
     PP_STRIP_HW_F(uint8_t, 8, 1)
 }

@@ -2,14 +2,14 @@
 # Usage: bash tools/check_spills.sh [-a]   (prints instances with spills, or all with -a)
 set -e
 cd "$(dirname "$0")/../processing-chain_amd"
-for f in strip_u16 strip_u16_chain strip_u8 strip_u8_chain; do
+for f in strip_u16 strip_u16_chain strip_u8 strip_u8_chain strip_u16_fused strip_u8_fused; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -x hip csrc/$f.hip --cuda-device-only -S -o /tmp/$f.s 2>/dev/null &
 done
 wait
 python3 - "$@" <<'PY'
 import re, sys
 bad = 0
-for f in ['/tmp/strip_u16.s', '/tmp/strip_u16_chain.s', '/tmp/strip_u8.s', '/tmp/strip_u8_chain.s']:
+for f in ["/tmp/strip_u16.s", "/tmp/strip_u16_chain.s", "/tmp/strip_u8.s", "/tmp/strip_u8_chain.s", "/tmp/strip_u16_fused.s", "/tmp/strip_u8_fused.s"]:
     txt = open(f).read()
     for b in txt.split('  - .agpr_count:')[1:]:
         name = re.search(r"\.name:\s+(\S+)", b).group(1)
@@ -34,7 +34,7 @@ wait
 python3 - <<'PY'
 import re
 bad = []
-for f in ['scale', 'cpvs', 'pack', 'siti', 'strip_u16', 'strip_u16_chain', 'strip_u8', 'strip_u8_chain']:
+for f in ["scale", "cpvs", "pack", "siti", "strip_u16", "strip_u16_chain", "strip_u8", "strip_u8_chain", "strip_u16_fused", "strip_u8_fused"]:
     txt = open('/tmp/%s.s' % f).read()
     for b in txt.split('  - .agpr_count:')[1:]:
         name = re.search(r"\.name:\s+(\S+)", b).group(1)
@@ -47,7 +47,7 @@ print("kernels with a private segment:", len(bad))
 PY
 # v_ashr_pk_u8_i32 keeps its destination's high half: a kernel that ORs more bytes
 # into such a result is wrong (cpvs.hip hit this); flag every occurrence
-if grep -l "v_ashr_pk_u8_i32" /tmp/scale.s /tmp/cpvs.s /tmp/pack.s /tmp/siti.s /tmp/strip_u16.s /tmp/strip_u16_chain.s /tmp/strip_u8.s /tmp/strip_u8_chain.s; then
+if grep -l "v_ashr_pk_u8_i32" /tmp/scale.s /tmp/cpvs.s /tmp/pack.s /tmp/siti.s /tmp/strip_u16.s /tmp/strip_u16_chain.s /tmp/strip_u8.s /tmp/strip_u8_chain.s /tmp/strip_u16_fused.s /tmp/strip_u8_fused.s; then
   echo "v_ashr_pk_u8_i32 present: check its uses"; exit 1
 fi
 echo "no v_ashr_pk_u8_i32"
