@@ -130,10 +130,16 @@ constexpr int strip_chain_min_waves() {
 #ifndef PIXPATH_LUMA9_WAVES
 #define PIXPATH_LUMA9_WAVES 6
 #endif
-// FUSE 9 (a chain's luma launch alone): its own budget where the window is narrow
+#ifndef PIXPATH_CHROMA11_WAVES
+#define PIXPATH_CHROMA11_WAVES 6
+#endif
+// FUSE 9 / 11 (a chain's luma / chroma launch alone): their own budgets where
+// the window is narrow
 template <int HW, int VTM, int FUSE>
 constexpr int strip_fused_min_waves() {
-    return FUSE == 9 && HW <= 4 && VTM <= 3 ? PIXPATH_LUMA9_WAVES : strip_chain_min_waves<HW, VTM>();
+    return FUSE == 9 && HW <= 4 && VTM <= 3    ? PIXPATH_LUMA9_WAVES
+           : FUSE == 11 && HW <= 4 && VTM <= 3 ? PIXPATH_CHROMA11_WAVES
+                                               : strip_chain_min_waves<HW, VTM>();
 }
 // Instances with register room for the clamped V-pass copy (a second
 // instantiation of the row loop): the rest keep the per-lane path rather than
