@@ -1339,9 +1339,13 @@ int launch_chain_planes(pp_scale_plan *P, const pp::PlaneJob *const *jobs, const
     const int vtm = strip_vtm_bucket(vtp);
     // the luma launch of a 10-bit chain (fuse 1 into 10 bits) takes its own
     // instance without the ring2 / second-stage code (FUSE 9)
-    const bool l9 = luma_only && P->chain_out == 10 && jobs[0]->fuse == 1 && !PP_KNOB("PIXPATH_CHAIN_NO_LUMA9");
+    // (clamped plans only: every plane's width a multiple of 4 with vector
+    // stores, so those instances compile the clamped V pass alone)
+    bool clamped = a.vec_dst != 0;
+    for (int i = 0; i < np; ++i) clamped = clamped && (jobs[i]->dw & 3) == 0;
+    const bool l9 = clamped && luma_only && P->chain_out == 10 && jobs[0]->fuse == 1 && !PP_KNOB("PIXPATH_CHAIN_NO_LUMA9");
     // ... and the chroma launch (every plane fuse 2) FUSE 11
-    bool c11 = !luma_only && P->luma && P->chain_out == 10 && !PP_KNOB("PIXPATH_CHAIN_NO_CHROMA11");
+    bool c11 = clamped && !luma_only && P->luma && P->chain_out == 10 && !PP_KNOB("PIXPATH_CHAIN_NO_CHROMA11");
     for (int i = 0; i < np; ++i) c11 = c11 && jobs[i]->fuse == 2;
     const bool u8 = P->si.depth == 8;
     KernelFn k = l9 ? (u8 ? pick_strip_luma_u8(hw, vtm) : pick_strip_luma_u16(hw, vtm))

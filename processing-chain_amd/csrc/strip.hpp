@@ -131,7 +131,7 @@ constexpr int strip_chain_min_waves() {
 #define PIXPATH_LUMA9_WAVES 6
 #endif
 #ifndef PIXPATH_CHROMA11_WAVES
-#define PIXPATH_CHROMA11_WAVES 6
+#define PIXPATH_CHROMA11_WAVES 7
 #endif
 // FUSE 9 / 11 (a chain's luma / chroma launch alone): their own budgets where
 // the window is narrow
@@ -563,7 +563,11 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
             default: if constexpr (VTM >= 8) vpass(std::integral_constant<int, 8>{}, cl_c); break;
             }
         };
-        if constexpr (FUSE != 1 && strip_clamp_path<ST, OUTB, HW, VTM, FUSE>()) {
+        if constexpr (FUSE == 9 || FUSE == 11) {
+            // the host picks these instances only for clamped plans (every
+            // plane's width a multiple of 4, vector stores): one copy of the loop
+            vdispatch(std::true_type{});
+        } else if constexpr (FUSE != 1 && strip_clamp_path<ST, OUTB, HW, VTM, FUSE>()) {
             if (clamp) vdispatch(std::true_type{});
             else vdispatch(std::false_type{});
         } else {
@@ -653,7 +657,9 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
                     default: pass2(std::integral_constant<int, 3>{}, cl_c); break;
                     }
                 };
-                if constexpr (strip_clamp_path<ST, OUTB, HW, VTM, FUSE>()) {
+                if constexpr (FUSE == 11) {
+                    dispatch2(std::true_type{});
+                } else if constexpr (strip_clamp_path<ST, OUTB, HW, VTM, FUSE>()) {
                     if (clamp) dispatch2(std::true_type{});
                     else dispatch2(std::false_type{});
                 } else {
