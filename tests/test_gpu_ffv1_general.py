@@ -156,3 +156,21 @@ def test_ragged_and_444_streams(gpu, fmt, fid, bits, hs, vs, w, h, grid):
     dec = ffv1.Ffv1Decoder(ref.gen_extradata(pf), w, h, max_frames=11, device=gpu)
     assert dec.fmt.name == fmt
     _check(dec.decode(b"".join(pkts), [len(p) for p in pkts]).to_numpy(), frames)
+
+
+@pytest.mark.parametrize("bounds", [[1, 2, 4, 8, 16], [3, 8, 32], [2, 6, 16, 48], [1], [1, 3, 8, 24, 64]],
+                         ids=["round4_666", "t3_8_32", "t2_6_16_48", "t1", "t1_3_8_24_64"])
+@pytest.mark.parametrize("name,fid,bits,hs,vs", FMTS[:2], ids=[f[0] for f in FMTS[:2]])
+def test_threshold_quantiser_streams_take_the_pixpath_path(gpu, bounds, name, fid, bits, hs, vs):
+    """pixpath-form records with any threshold quantiser -- round 4's files
+    (min(5, bit length), 666 contexts) and other sets -- decode through the
+    one-line-row path with the thresholds read back from the record (the
+    first quantiser as ALU compares): every frame exact."""
+    from pixpath import ffv1
+    w, h = 480, 270
+    t = ref._runs(bounds)
+    pf = ref.make_prof(bits, hs, vs, 8, 4, [[t, t, t, ref.ZERO, ref.ZERO]], tidx=(0, 0), coder=1, gop=1)
+    frames, pkts = _sequence(pf, fid, w, h, 6, len(bounds) + bits)
+    dec = ffv1.Ffv1Decoder(ref.gen_extradata(pf), w, h, max_frames=6, device=gpu)
+    assert dec.info["pixpath_tables"] == 1
+    _check(dec.decode(b"".join(pkts), [len(p) for p in pkts]).to_numpy(), frames)
