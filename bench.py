@@ -779,7 +779,10 @@ def bench_stall(args, rank, world, dev):
     ops.spinner_upload(anim, "yuv422p10le", device=dev.index)
     src, _ = make_inputs(("yuv422p10le", w, h, None, 0, 0, None, None), 8, 404 + rank, dev)
     dst = FrameBatch("yuv422p10le", w, h, n, device=dev)
-    src_idx = np.arange(n, dtype=np.int32) % 8
+    # as the product composes a stall run (pixpath/stall.py, PP-STALL-1): ONE
+    # frozen frame repeated, the spinner animating over it (round 5 cycled 8
+    # source frames, which the L2 held: VERDICT r5 item 7)
+    src_idx = np.zeros(n, dtype=np.int32)
     sp_idx = np.arange(n, dtype=np.int32) % len(anim)
     ev = []
     for i in range(args.warmup + args.steps):
@@ -793,6 +796,10 @@ def bench_stall(args, rank, world, dev):
     ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
     fb = frame_bytes("yuv422p10le", w, h)
     achieved = 2 * fb * n / (ms / 1000.0) / 1e9
+    # the honest HBM figure of a stall run: its write stream (the frozen frame
+    # is read once per launch), against the measured store ceiling of the box
+    # (contiguous dwordx4 stores, profiles/r2/strip_experiments.md: 6,774 GB/s)
+    write_gbs = fb * n / (ms / 1000.0) / 1e9
     # the long test's canvases (create_avpvs_segment): 720p yuv420p10le segment
     # frames -> overlay yuv420p -> yuv422p10le 1080p, one chain-plan launch
     seg = FrameBatch("yuv420p10le", 1280, 720, n, device=dev)
@@ -827,7 +834,11 @@ def bench_stall(args, rank, world, dev):
                           "roofline": {"bound": "hbm", "kernel": "stall_kernel", "achieved": round(achieved, 1),
                                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                                        "traffic": None, "algorithmic_bytes_per_launch": 2 * fb * n,
-                                       "avg_launch_ms": round(ms, 4)},
+                                       "avg_launch_ms": round(ms, 4),
+                                       "note": "SURVEY 8d bytes (read + write per frame); the frozen frame is "
+                                               "read from HBM once per launch, so write_gbs is the HBM figure"},
+                          "write_gbs": round(write_gbs, 1), "write_frac_of_store_ceiling": round(write_gbs / 6774.0, 4),
+                          "write_frac_of_peak": round(write_gbs / HBM_PEAK_GBS, 4),
                           "canvas_chain": canvas, "cpu_baseline": None, "library": library_id(),
                           "tuning_overrides": tuning_overrides() or None}), flush=True)
     return 0
@@ -953,15 +964,20 @@ def bench_ffv1(args, rank, world, dev):
 
 
 def reference_stream_decode(args, src, dev, ffv1_ref):
-    """GPU decode of an AVPVS in the reference's own FFV1 shape
+    """GPU decode of AVPVSes in the reference's own FFV1 shape
     (`-threads 4 -level 3 -coder 1 -context 1`, /root/reference/lib/ffmpeg.py:993:
     2x2 slices, -context 1's 5-input set, a transmitted state table, GOPs of 12
     with states carried).  The oracle's general encoder writes one GOP of the
-    bench content (input generation, untimed; FFmpeg is absent); the GPU decodes
-    that GOP repeated 50 times (600 frames = 200 slice chains, one lane each),
-    checked lossless; the oracle's own decode of the GOP is the CPU row.  A
-    chain is one slice over a whole GOP, so this stream has 200 serial chains
-    where pixpath's 8x8 intra stream has 38,400."""
+    bench content (input generation, untimed; FFmpeg is absent); a stream is
+    that GOP repeated 50 times (600 frames = 200 slice chains, one lane each).
+    A chain is one slice over a whole GOP, so one stream has 200 serial chains
+    where pixpath's 8x8 intra stream has 38,400: it decodes slower than the
+    host's cores.  K streams decoded in ONE launch (pp_ffv1_decode_group, as
+    the reference's ParallelRunner feeds the CPVS stage several PVSes at once)
+    fill the SIMDs: frames/s at K = 1, 4, 16, each checked lossless, beside
+    the oracle's general decoder on 1 and 16 host threads (one GOP per thread,
+    threads in parallel: ctypes releases the GIL)."""
+    import threading
     import time
     import numpy as np
     import torch
@@ -977,39 +993,65 @@ def reference_stream_decode(args, src, dev, ffv1_ref):
     genc = ffv1_ref.GenEncoder(pf, w, h)
     pkts = [genc.encode(f) for f in frames]
     extra = ffv1_ref.gen_extradata(pf)
-    gdec = ffv1_ref.GenDecoder(extra, w, h)
-    t0 = time.perf_counter()
-    cpu_ok = True
-    for f, p in zip(frames, pkts):
-        rc, planes, _ = gdec.decode(p)
-        cpu_ok = cpu_ok and rc == 0 and all(np.array_equal(planes[q], f[q]) for q in range(3))
-    cdt = time.perf_counter() - t0
+
+    def cpu_decode(nthreads):
+        ok = [True] * nthreads
+
+        def one(t):
+            gdec = ffv1_ref.GenDecoder(extra, w, h)
+            for f, p in zip(frames, pkts):
+                rc, planes, _ = gdec.decode(p)
+                ok[t] = ok[t] and rc == 0 and all(np.array_equal(planes[q], f[q]) for q in range(3))
+        ths = [threading.Thread(target=one, args=(t,)) for t in range(nthreads)]
+        t0 = time.perf_counter()
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        return {"frames_per_s": round(nthreads * gop / (time.perf_counter() - t0), 3), "threads": nthreads,
+                "lossless": all(ok)}
+    cpu = [cpu_decode(1), cpu_decode(16)]
     m = reps * gop
     one = np.frombuffer(b"".join(pkts), np.uint8)
     data = torch.from_numpy(np.tile(one, reps)).pin_memory().numpy()
     sizes = np.tile(np.array([len(p) for p in pkts], np.int64), reps)
-    dec = ffv1.Ffv1Decoder(extra, w, h, max_frames=m, device=dev)
-    back = FrameBatch("yuv422p10le", w, h, m, device=dev)
-    dec.decode(data, sizes, dst=back)  # warm-up
-    torch.cuda.synchronize()
-    steps = max(1, min(args.steps, 2))
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        dec.reset()
-        dec.decode(data, sizes, dst=back)
-    torch.cuda.synchronize()
-    ddt = (time.perf_counter() - t0) / steps
-    ok = all(bool(torch.equal(back.view(p)[r * gop:(r + 1) * gop], src.view(p)[:gop]))
-             for p in range(3) for r in (0, reps - 1))
-    return {"frames_per_s": round(m / ddt, 1), "ms_per_step": round(ddt * 1e3, 3), "frames": m, "lossless": ok,
-            "slices": [2, 2], "gop": gop, "chains": reps * 4, "slices_per_workgroup": dec.slices_per_workgroup,
+    fb = frame_bytes("yuv422p10le", w, h)
+    rows = []
+    decs = []
+    for K in (1, 4, 16):
+        free = torch.cuda.mem_get_info(dev)[0]
+        if K * m * (fb + len(one) / gop) * 1.2 > 0.5 * free:
+            rows.append({"streams": K, "skipped": "needs %.1f GB of HBM" % (K * m * fb / 1e9)})
+            continue
+        while len(decs) < K:
+            decs.append(ffv1.Ffv1Decoder(extra, w, h, max_frames=m, device=dev))
+        back = FrameBatch("yuv422p10le", w, h, K * m, device=dev)
+        ffv1.decode_group(decs[:K], [data] * K, [sizes] * K, dst=back)  # warm-up (workspace growth)
+        torch.cuda.synchronize()
+        steps = max(1, min(args.steps, 2))
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            for d in decs[:K]:
+                d.reset()
+            ffv1.decode_group(decs[:K], [data] * K, [sizes] * K, dst=back)
+        torch.cuda.synchronize()
+        ddt = (time.perf_counter() - t0) / steps
+        ok = all(bool(torch.equal(back.view(p)[k * m + r * gop:k * m + (r + 1) * gop], src.view(p)[:gop]))
+                 for p in range(3) for k in (0, K - 1) for r in (0, reps - 1))
+        rows.append({"streams": K, "frames_per_s": round(K * m / ddt, 1), "ms_per_step": round(ddt * 1e3, 3),
+                     "chains": K * reps * 4, "lossless": ok})
+        del back
+        torch.cuda.empty_cache()
+    best = max((r["frames_per_s"] for r in rows if "frames_per_s" in r), default=None)
+    return {"frames_per_s": rows[0].get("frames_per_s"), "streams": rows, "frames": m,
+            "slices": [2, 2], "gop": gop, "chains_per_stream": reps * 4,
+            "slices_per_workgroup": decs[0].slices_per_workgroup if decs else None,
             "bytes_per_frame": round(len(one) / gop, 1),
-            "cpu_oracle": {"frames_per_s": round(gop / cdt, 3), "cores": 1, "lossless": cpu_ok,
-                           "sample": "one GOP of %d frames, oracle/ffv1_oracle.c general decoder" % gop},
-            "note": "oracle-encoded GOP (FFmpeg's -coder 1 -context 1 shape) repeated %dx; "
-                    "packets from pinned host memory (H2D included); FFmpeg's own files unpinned" % reps}
-
-
+            "cpu_oracle": cpu[0], "cpu_oracle_16": cpu[1],
+            "gpu_best_vs_cpu_16": round(best / cpu[1]["frames_per_s"], 3) if best else None,
+            "note": "oracle-encoded GOP (FFmpeg's -coder 1 -context 1 shape) repeated %dx per stream; K streams in "
+                    "one pp_ffv1_decode_group launch; packets from pinned host memory (H2D included); CPU: the "
+                    "oracle's general decoder, one GOP per thread; FFmpeg's own files unpinned" % reps}
 
 
 if __name__ == "__main__":

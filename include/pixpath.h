@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PP_ABI_VERSION 6
+#define PP_ABI_VERSION 7
 
 /* return codes */
 #define PP_OK 0
@@ -315,6 +315,20 @@ int pp_ffv1_decode(pp_ffv1_dec *dec, const uint8_t *packets, const int64_t *fram
 int pp_ffv1_decoder_info(const pp_ffv1_dec *dec, int *info, int n);
 int pp_ffv1_decoder_reset(pp_ffv1_dec *dec);
 int pp_ffv1_decoder_geometry(const pp_ffv1_dec *dec, int *slices_per_workgroup, int *row_cap);
+/* ABI v7.  One launch over n streams of ONE configuration record (equal
+ * extradata, size and context): decs[k] decodes stream k -- nframes[k]
+ * packets back to back in host memory at packets[k], sizes frame_sizes[k] --
+ * into dst frames [nframes[0] + ... + nframes[k-1], ...) of the one device
+ * batch dst, each stream continuing / keeping its own carried GOP states as
+ * pp_ffv1_decode does.  The slice chains of an FFmpeg-made AVPVS are few
+ * (GOP 12 at 2x2 slices: 200 per 600 frames, one lane each); several
+ * streams' chains side by side are what fill the SIMDs -- the reference's
+ * ParallelRunner feeds the CPVS stage several PVSes at once
+ * (lib/cmd_utils.py:93-101).  decs[0] holds the launch workspace; the
+ * decoders' workspaces grow on demand to what a call needs.  Synchronises
+ * `stream`; on a slice error the message names the stream. */
+int pp_ffv1_decode_group(pp_ffv1_dec *const *decs, int n, const uint8_t *const *packets,
+                         const int64_t *const *frame_sizes, const int *nframes, const pp_frames *dst, void *stream);
 
 #ifdef __cplusplus
 }

@@ -244,7 +244,9 @@ __global__ __launch_bounds__(256) void ffv1_model_kernel(const Ffv1Args a) {
         if (x0) __syncthreads();  // the previous chunk's LDS reads are done
         // stage columns x0 - 1 .. x0 + 64 of the row above and the row of every
         // lane (segment = lane j, row rw) as 16-byte pieces of the aligned span
-        // x0 - 8 .. x0 + 72: thread t takes pieces t, t + 256, ... of the
+        // x0 - SP .. x0 + 64 + SP (SP samples per piece: x0 is a multiple of
+        // 64, so every piece of a 16-byte aligned row is 16-byte aligned --
+        // 8-bit pieces started 8 bytes off): thread t takes pieces t, t + 256, ... of the
         // chunk, so consecutive threads read consecutive bytes of one slice row
         // (a per-thread walk of 2-byte loads, one row per lane, was bound by
         // the L1 -> L2 requests: 3.3e9 per 600 frames, profiles/r5/ffv1_pmc.txt).
@@ -252,12 +254,12 @@ __global__ __launch_bounds__(256) void ffv1_model_kernel(const Ffv1Args a) {
         // sample by sample with the bounds check (zeros outside the row).
         {
             constexpr int SP = 16 / (int)sizeof(ST);  // samples per piece
-            constexpr int NP = (kMX + 16) / SP;       // pieces per segment
+            constexpr int NP = (kMX + 2 * SP) / SP;   // pieces per segment
             for (int i = t; i < 128 * NP; i += 256) {
                 const int seg = i / NP, pc = i - seg * NP, j = seg >> 1, rw = seg & 1;
                 const ST *rp = reinterpret_cast<const ST *>(s_ptr[j][rw]);
                 const int lim = (rw || s_info[j][1]) ? s_info[j][0] : 0;  // row above absent: zeros
-                const int s0 = x0 - 8 + pc * SP;
+                const int s0 = x0 - SP + pc * SP;
                 int *dst = s_row + j * kMLane + rw * kMS + (s0 - (x0 - 1));  // column of sample s0
                 ST v[SP];
                 if (s0 >= 0 && s0 + SP <= lim && (reinterpret_cast<uintptr_t>(rp) & 15) == 0) {

@@ -555,8 +555,14 @@ struct pp_ffv1_dec {
     int16_t *dquant = nullptr;
     uint4 *dinit = nullptr;
     int init_off[kFfv1MaxTables];
+    // decode workspace, grown on demand to what a call needs (a
+    // record with thousands of contexts no longer reserves per * max_frames
+    // chain slots up front -- a GOP-12 stream needs a twelfth of them)
     int64_t slots = 0;        // chain state slots allocated (64-aligned)
+    int64_t ns_cap = 0;       // slice entries (soff / slen / status)
+    int64_t gop_cap = 0;      // GOP entries
     bool carry_valid = false; // `carry` holds the last GOP's states of the previous decode
+    std::vector<uint8_t> extra;  // the configuration record (a group decode needs equal ones)
 };
 
 namespace {
@@ -638,16 +644,10 @@ extern "C" int pp_ffv1_decoder_create(pp_ctx *ctx, const uint8_t *extra, int ext
         return PP_OK;
     }
     const int per = R.nh * R.nv;
-    D->slots = ((int64_t)per * max_frames + 63) / 64 * 64;
-    const int64_t half = 2 * (int64_t)R.max_ctx * 16 * D->slots;
+    D->extra.assign(extra, extra + extra_size);
     const int64_t chalf = 2 * (int64_t)R.max_ctx * 16 * ((per + 63) / 64 * 64);
     PP_HIP(hipSetDevice(ctx->device));
-    PP_HIP(hipMalloc(&D->states, 2 * half));  // both halves
-    PP_HIP(hipMalloc(&D->carry, 2 * chalf));
-    PP_HIP(hipMalloc(&D->soff, sizeof(int64_t) * per * max_frames));
-    PP_HIP(hipMalloc(&D->slen, sizeof(int64_t) * per * max_frames));
-    PP_HIP(hipMalloc(&D->status, sizeof(int) * per * max_frames));
-    PP_HIP(hipMalloc(&D->gop, sizeof(int) * 3 * max_frames));
+    PP_HIP(hipMalloc(&D->carry, 2 * chalf));  // the decode workspace itself is allocated by the first decode
     PP_HIP(hipMalloc(&D->tables, 512 + 1024 + 128));
     PP_HIP(hipMalloc(&D->dquant, qbytes));
     uint8_t tab[512 + 1024 + 128];
@@ -732,33 +732,84 @@ extern "C" int pp_ffv1_decoder_reset(pp_ffv1_dec *D) {
     return PP_OK;
 }
 
-extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int64_t *frame_sizes, int nframes,
-                              const pp_frames *dst, void *stream) {
-    if (!D || !packets || !frame_sizes || !dst || nframes < 0) PP_FAIL(PP_ERR_INVALID, "null argument");
-    if (!D->ctx) PP_FAIL(PP_ERR_INVALID, "host-only decoder cannot decode");
-    if (nframes > D->max_frames) PP_FAIL(PP_ERR_INVALID, "%d frames > max_frames %d", nframes, D->max_frames);
-    if (nframes == 0) return PP_OK;
+namespace {
+
+// grow a device array to at least `need` elements (the decode is synchronous,
+// so no earlier launch still uses the old one)
+template <typename T>
+hipError_t grow(T **p, int64_t *cap, int64_t need) {
+    if (need <= *cap) return hipSuccess;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipError_t e = hipMalloc(p, sizeof(T) * need)) return e;
+    *cap = need;
+    return hipSuccess;
+}
+
+}  // namespace
+
+// One launch over the slice chains of n streams of one configuration record
+// (decs[k] decodes stream k: its packets, sizes and frame count; its carried
+// GOP states in and out).  Stream k's frames land at dst frames
+// [sum nframes[<k], ...).  The chains of one stream are few when its GOPs are
+// long (FFmpeg's GOP 12 at 2x2 slices: 200 per 600 frames, one lane each), so
+// several streams side by side are what fill the SIMDs.  decs[0] owns the
+// launch workspace.
+static int decode_group(pp_ffv1_dec *const *decs, int n, const uint8_t *const *packets,
+                        const int64_t *const *frame_sizes, const int *nframes, const pp_frames *dst, void *stream) {
+    if (!decs || n < 1 || !packets || !frame_sizes || !nframes || !dst) PP_FAIL(PP_ERR_INVALID, "null argument");
+    pp_ffv1_dec *D = decs[0];
+    for (int k = 0; k < n; ++k) {
+        const pp_ffv1_dec *E = decs[k];
+        if (!E || !packets[k] || !frame_sizes[k] || nframes[k] < 0) PP_FAIL(PP_ERR_INVALID, "null argument (stream %d)", k);
+        if (!E->ctx) PP_FAIL(PP_ERR_INVALID, "host-only decoder cannot decode");
+        if (nframes[k] > E->max_frames) PP_FAIL(PP_ERR_INVALID, "%d frames > max_frames %d", nframes[k], E->max_frames);
+        for (int j = 0; j < k; ++j)
+            if (decs[j] == E) PP_FAIL(PP_ERR_INVALID, "decoder of stream %d given twice", k);
+        if (E->ctx != D->ctx || E->w != D->w || E->h != D->h || E->extra != D->extra)
+            PP_FAIL(PP_ERR_INVALID, "stream %d: a group decode needs one configuration record, size and context", k);
+    }
     const Ffv1Record &R = D->rec;
     hipStream_t st = static_cast<hipStream_t>(stream);
     PP_HIP(hipSetDevice(D->ctx->device));
-    const int per = R.nh * R.nv, ns = per * nframes;
-    std::vector<int64_t> soff(ns), slen(ns);
-    int64_t base = 0;
+    const int per = R.nh * R.nv;
+    int64_t ftot = 0;
+    for (int k = 0; k < n; ++k) ftot += nframes[k];
+    if (ftot == 0) return PP_OK;
+    const int64_t ns = per * ftot;
+    std::vector<int64_t> soff(ns), slen(ns), bytes(n);
+    std::vector<int> gop, first_gop(n), ngop(n);
+    std::vector<char> carry_in(n);
     std::string err;
-    const bool carry_in = D->carry_valid;
-    D->carry_valid = false;  // until this decode has succeeded
-    if (int rc = ffv1_slice_table(packets, frame_sizes, nframes, per, R.ec, soff.data(), slen.data(), &base, &err))
-        PP_FAIL(rc, "%s", err.c_str());
-    // GOPs: a keyframe starts one; frame 0 without one continues the previous decode's
-    std::vector<int> gop;
-    for (int f = 0; f < nframes; ++f) {
-        const int key = ffv1_keyframe_bit(packets + soff[(int64_t)f * per], slen[(int64_t)f * per]);
-        if (f == 0 || key) {
-            if (f == 0 && !key && !carry_in)
-                PP_FAIL(PP_ERR_INVALID, "frame 0 is not a keyframe and no earlier frame of its GOP was decoded");
-            gop.insert(gop.end(), {f, 0, key});
+    int64_t base = 0, f0 = 0;
+    for (int k = 0; k < n; ++k) {  // slice tables and GOPs, stream by stream
+        pp_ffv1_dec *E = decs[k];
+        carry_in[k] = E->carry_valid;
+        first_gop[k] = (int)gop.size() / 3;
+        const int nf = nframes[k];
+        if (nf == 0) continue;
+        E->carry_valid = false;  // until this decode has succeeded
+        int64_t sb = 0;
+        if (int rc = ffv1_slice_table(packets[k], frame_sizes[k], nf, per, R.ec, soff.data() + f0 * per,
+                                      slen.data() + f0 * per, &sb, &err))
+            PP_FAIL(rc, "stream %d: %s", k, err.c_str());
+        for (int64_t i = f0 * per; i < (f0 + nf) * per; ++i) soff[i] += base;
+        for (int f = 0; f < nf; ++f) {  // a keyframe starts a GOP; frame 0 without one continues the carried one
+            const int64_t s0 = (f0 + f) * per;
+            const int key = ffv1_keyframe_bit(packets[k] + soff[s0] - base, slen[s0]);
+            if (f == 0 || key) {
+                if (f == 0 && !key && !carry_in[k])
+                    PP_FAIL(PP_ERR_INVALID, "stream %d: frame 0 is not a keyframe and no earlier frame of its GOP "
+                                            "was decoded", k);
+                gop.insert(gop.end(), {(int)(f0 + f), 0, key});
+            }
+            gop[gop.size() - 2]++;
         }
-        gop[gop.size() - 2]++;
+        ngop[k] = (int)gop.size() / 3 - first_gop[k];
+        bytes[k] = sb;
+        base += (sb + 63) & ~int64_t(63);
+        f0 += nf;
     }
     const int ngops = (int)gop.size() / 3, nchains = ngops * per;
     if (base > D->pkt_cap) {
@@ -768,23 +819,45 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
         PP_HIP(hipMalloc(&D->pkt, base + 64));  // the bytestream window reads up to 8 B past a slice
         D->pkt_cap = base;
     }
-    PP_HIP(hipMemcpyAsync(D->pkt, packets, base, hipMemcpyHostToDevice, st));
+    const int64_t sb = 2 * (int64_t)R.max_ctx * 16;  // one half, per chain
+    const int64_t need_slots = ((int64_t)nchains + 63) / 64 * 64;
+    if (need_slots > D->slots) {
+        if (D->states) PP_HIP(hipFree(D->states));
+        D->states = nullptr;
+        D->slots = 0;
+        PP_HIP(hipMalloc(&D->states, 2 * sb * need_slots));  // both halves
+        D->slots = need_slots;
+    }
+    if (ns > D->ns_cap) {  // soff / slen / status share one capacity
+        int64_t c = 0;
+        D->ns_cap = 0;
+        PP_HIP(grow(&D->soff, &c, ns));
+        c = 0;
+        PP_HIP(grow(&D->slen, &c, ns));
+        c = 0;
+        PP_HIP(grow(&D->status, &c, ns));
+        D->ns_cap = ns;
+    }
+    PP_HIP(grow(&D->gop, &D->gop_cap, (int64_t)gop.size()));
+    for (int64_t k = 0, off = 0; k < n; off += (bytes[k] + 63) & ~int64_t(63), ++k)
+        if (bytes[k]) PP_HIP(hipMemcpyAsync(D->pkt + off, packets[k], bytes[k], hipMemcpyHostToDevice, st));
     PP_HIP(hipMemcpyAsync(D->soff, soff.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
     PP_HIP(hipMemcpyAsync(D->slen, slen.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
     PP_HIP(hipMemcpyAsync(D->gop, gop.data(), sizeof(int) * gop.size(), hipMemcpyHostToDevice, st));
     PP_HIP(hipMemsetAsync(D->status, 0, sizeof(int) * ns, st));
-    const int64_t sb = 2 * (int64_t)R.max_ctx * 16;  // one half, per chain
-    const int64_t half = sb * D->slots, used = sb * ((nchains + 63) / 64 * 64);
+    const int64_t half = sb * D->slots, used = sb * need_slots;
     const int64_t chalf = sb * ((per + 63) / 64 * 64);
     PP_HIP(hipMemsetAsync(D->states, 128, used, st));
     PP_HIP(hipMemsetAsync(D->states + half, 128, used, st));
     auto copy_states = [&](const uint8_t *src, int64_t sh, int s0, uint8_t *dstp, int64_t dh, int d0) {
-        const int64_t n = 2 * (int64_t)per * 2 * R.max_ctx;
-        hipLaunchKernelGGL(ffv1_state_copy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, sh, s0,
+        const int64_t m = 2 * (int64_t)per * 2 * R.max_ctx;
+        hipLaunchKernelGGL(ffv1_state_copy_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, src, sh, s0,
                            dstp, dh, d0, per, 2 * R.max_ctx);
         return hipGetLastError();
     };
-    if (!gop[2]) PP_HIP(copy_states(D->carry, chalf, 0, D->states, half, 0));  // GOP 0 continues the carried states
+    for (int k = 0; k < n; ++k)  // a stream whose first GOP continues its carried states
+        if (ngop[k] && !gop[3 * first_gop[k] + 2])
+            PP_HIP(copy_states(decs[k]->carry, chalf, 0, D->states, half, first_gop[k] * per));
     Ffv1DecArgs a{};
     a.pkt = D->pkt; a.soff = D->soff; a.slen = D->slen;
     for (int p = 0; p < 3; ++p) {
@@ -829,14 +902,32 @@ extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int6
     else
         hipLaunchKernelGGL((ffv1_decode_kernel<1, false>), grid, block, lds, st, a);
     PP_HIP(hipGetLastError());
-    // the last GOP's states, for a next decode that continues it
-    PP_HIP(copy_states(D->states, half, (ngops - 1) * per, D->carry, chalf, 0));
+    // each stream's last GOP states, for its next decode that continues it
+    for (int k = 0; k < n; ++k)
+        if (ngop[k]) PP_HIP(copy_states(D->states, half, (first_gop[k] + ngop[k] - 1) * per, decs[k]->carry, chalf, 0));
     std::vector<int> status(ns);
     PP_HIP(hipMemcpyAsync(status.data(), D->status, sizeof(int) * ns, hipMemcpyDeviceToHost, st));
     PP_HIP(hipStreamSynchronize(st));
     static const char *what[] = {"ok", "slice CRC mismatch", "bad slice header", "bytestream end mismatch"};
-    for (int i = 0; i < ns; ++i)
-        if (status[i]) PP_FAIL(PP_ERR_INVALID, "frame %d slice %d: %s", i / per, i % per, what[std::min(status[i], 3)]);
-    D->carry_valid = true;
+    for (int64_t i = 0, fk = 0, k = 0; i < ns; ++i) {
+        while (k < n && i >= (fk + nframes[k]) * per) fk += nframes[k++];
+        if (status[i])
+            PP_FAIL(PP_ERR_INVALID, "%sframe %d slice %d: %s", n > 1 ? ("stream " + std::to_string(k) + ": ").c_str() : "",
+                    (int)(i / per - fk), (int)(i % per), what[std::min(status[i], 3)]);
+    }
+    for (int k = 0; k < n; ++k)
+        if (nframes[k]) decs[k]->carry_valid = true;
     return PP_OK;
+}
+
+extern "C" int pp_ffv1_decode(pp_ffv1_dec *D, const uint8_t *packets, const int64_t *frame_sizes, int nframes,
+                              const pp_frames *dst, void *stream) {
+    if (!D || !packets || !frame_sizes || !dst || nframes < 0) PP_FAIL(PP_ERR_INVALID, "null argument");
+    return decode_group(&D, 1, &packets, &frame_sizes, &nframes, dst, stream);
+}
+
+extern "C" int pp_ffv1_decode_group(pp_ffv1_dec *const *decs, int n, const uint8_t *const *packets,
+                                    const int64_t *const *frame_sizes, const int *nframes, const pp_frames *dst,
+                                    void *stream) {
+    return decode_group(decs, n, packets, frame_sizes, nframes, dst, stream);
 }

@@ -122,63 +122,79 @@ struct StallArgs {
     int nk, G;             // output frames in this launch, frames per tile
 };
 
+#ifndef PIXPATH_STALL_G
+#define PIXPATH_STALL_G 6
+#endif
 template <int EB>
 __global__ __launch_bounds__(kRowLanes) void stall_kernel(const StallArgs a) {
     using T = typename std::conditional<EB == 1, uint8_t, uint16_t>::type;
     constexpr int N = 16 / EB;
-    // units in tiles of G output frames: a tile walks the rows, each row of
-    // its G frames in turn, so a source row comes from the XCD's L2 for all
-    // but the first of them (G = 1: frame-major; G = all: row-major)
+    // a wave owns one row of one plane for a tile of G consecutive output
+    // frames: it loads the source row once (again only where the tile's
+    // source index changes: a stall run repeats ONE frozen frame) and stores
+    // it G times, blending the spinner row of each frame's spinner index in
+    // registers.  Units are tile-major with a tile's rows consecutive, so the
+    // waves in flight write adjacent rows of the same G frames.  (Round 5 and
+    // earlier: one wave per (row, frame) re-reading the row from L2 for each
+    // frame -- 3.0 TB/s of writes, wave dispatch rather than HBM the bound.)
     const int rows = a.pl[0].rows + a.pl[1].rows + a.pl[2].rows;
     const int unit = xcd_remap(blockIdx.x, gridDim.x);
-    const int tile = unit / (rows * a.G), wi = unit - tile * rows * a.G;
-    const int r = wi / a.G, frame = tile * a.G + (wi - r * a.G);
-    if (frame >= a.nk) return;
+    const int tile = unit / rows, r = unit - tile * rows;
+    const int f0 = tile * a.G, f1 = min(a.nk, f0 + a.G);
+    if (f0 >= a.nk) return;
     int p = 0, y = r;
     if (y >= a.pl[0].rows) { y -= a.pl[0].rows; p = 1; }
     if (p == 1 && y >= a.pl[1].rows) { y -= a.pl[1].rows; p = 2; }
     const RowPlane &g = a.pl[p];
-    const int si = a.idx[2 * frame], sp = a.idx[2 * frame + 1];
-    const T *srow = si >= 0 ? reinterpret_cast<const T *>(g.src + si * g.sfs + (int64_t)y * g.sls) : nullptr;
-    T *drow = reinterpret_cast<T *>(g.dst + frame * g.dfs + (int64_t)y * g.dls);
     // spinner plane geometry
     const int pw = p ? (a.sw >> a.hs) : a.sw, ph = p ? (a.sh >> a.vs) : a.sh;
     const int px0 = p ? (a.ox >> a.hs) : a.ox, py0 = p ? (a.oy >> a.vs) : a.oy;
     const int64_t ysz = (int64_t)a.sw * a.sh, csz = (int64_t)pw * ph;
-    const uint16_t *S = nullptr, *A = nullptr;
-    const bool in_rows = sp >= 0 && y >= py0 && y < py0 + ph;
-    if (in_rows) {
-        // layout per spinner frame: Y, Al (sw*sh each), then U, V, Ac (csz each)
-        const uint16_t *sbase = a.spin + (int64_t)sp * a.spin_stride;
-        S = (p == 0 ? sbase : sbase + 2 * ysz + (p == 2 ? csz : 0)) + (int64_t)(y - py0) * pw;
-        A = (p == 0 ? sbase + ysz : sbase + 2 * ysz + 2 * csz) + (int64_t)(y - py0) * pw;
-    }
+    const bool spin_row = y >= py0 && y < py0 + ph;
     const int chunks = (g.W + N - 1) / N;
     for (int q0 = threadIdx.x; q0 < chunks; q0 += kRowLanes * kRowUnroll) {
-        uint4 v[kRowUnroll];
+        uint4 base[kRowUnroll];
+        int cur = -2;  // no source row loaded (-1 is the black frame)
+        for (int f = f0; f < f1; ++f) {
+            const int si = a.idx[2 * f], sp = a.idx[2 * f + 1];
+            if (si != cur) {  // wave-uniform
+                cur = si;
+                const T *srow = si >= 0 ? reinterpret_cast<const T *>(g.src + si * g.sfs + (int64_t)y * g.sls) : nullptr;
 #pragma unroll
-        for (int u = 0; u < kRowUnroll; ++u) {
-            const int q = q0 + u * kRowLanes;
-            if (q < chunks) v[u] = shifted_chunk<T>(srow, q * N, 0, g.W, g.black, g.vec);
-        }
-#pragma unroll
-        for (int u = 0; u < kRowUnroll; ++u) {
-            const int q = q0 + u * kRowLanes, x = q * N;
-            if (q >= chunks) continue;
-            if (in_rows && x + N > px0 && x < px0 + pw) {
-                T e[N];
-                __builtin_memcpy(e, &v[u], 16);
-#pragma unroll
-                for (int i = 0; i < N; ++i) {
-                    const int sx = x + i - px0;
-                    if (sx >= 0 && sx < pw) {
-                        const int al = A[sx];
-                        e[i] = static_cast<T>((static_cast<int>(e[i]) * (255 - al) + static_cast<int>(S[sx]) * al + 127) / 255);
-                    }
+                for (int u = 0; u < kRowUnroll; ++u) {
+                    const int q = q0 + u * kRowLanes;
+                    if (q < chunks) base[u] = shifted_chunk<T>(srow, q * N, 0, g.W, g.black, g.vec);
                 }
-                __builtin_memcpy(&v[u], e, 16);
             }
-            put_chunk<T>(drow, x, g.W, g.dvec, v[u]);
+            T *drow = reinterpret_cast<T *>(g.dst + f * g.dfs + (int64_t)y * g.dls);
+            const uint16_t *S = nullptr, *A = nullptr;
+            const bool in_rows = sp >= 0 && spin_row;
+            if (in_rows) {
+                // layout per spinner frame: Y, Al (sw*sh each), then U, V, Ac (csz each)
+                const uint16_t *sbase = a.spin + (int64_t)sp * a.spin_stride;
+                S = (p == 0 ? sbase : sbase + 2 * ysz + (p == 2 ? csz : 0)) + (int64_t)(y - py0) * pw;
+                A = (p == 0 ? sbase + ysz : sbase + 2 * ysz + 2 * csz) + (int64_t)(y - py0) * pw;
+            }
+#pragma unroll
+            for (int u = 0; u < kRowUnroll; ++u) {
+                const int q = q0 + u * kRowLanes, x = q * N;
+                if (q >= chunks) continue;
+                uint4 v = base[u];
+                if (in_rows && x + N > px0 && x < px0 + pw) {
+                    T e[N];
+                    __builtin_memcpy(e, &v, 16);
+#pragma unroll
+                    for (int i = 0; i < N; ++i) {
+                        const int sx = x + i - px0;
+                        if (sx >= 0 && sx < pw) {
+                            const int al = A[sx];
+                            e[i] = static_cast<T>((static_cast<int>(e[i]) * (255 - al) + static_cast<int>(S[sx]) * al + 127) / 255);
+                        }
+                    }
+                    __builtin_memcpy(&v, e, 16);
+                }
+                put_chunk<T>(drow, x, g.W, g.dvec, v);
+            }
         }
     }
 }
@@ -343,11 +359,12 @@ extern "C" int pp_stall_compose(pp_ctx *ctx, int fmt, int w, int h, const pp_fra
         StallArgs b = a;
         for (int p = 0; p < 3; ++p) b.pl[p].dst += k0 * a.pl[p].dfs;
         b.nk = nk;
-        // 1080p10 stall frames: G = 1 1.34 ms, 2 1.09-1.12, 3 1.07-1.10, 4 1.12,
-        // 6 1.03-1.05, 8 1.33, 16 1.42, 64 1.55 (power-of-two tiles alias the
-        // frames' rows onto the same HBM channels)
-        b.G = 6;
-        const dim3 grid((unsigned)((nk + b.G - 1) / b.G * b.G * rows));
+        // frames per wave (one source load, G stores of the row).  Round 2,
+        // one wave per (row, frame) in tiles of G: G = 1 1.34 ms, 2
+        // 1.09-1.12, 3 1.07-1.10, 4 1.12, 6 1.03-1.05, 8 1.33, 16 1.42, 64 1.55
+        // (power-of-two tiles alias the frames' rows onto the same HBM channels)
+        b.G = PIXPATH_STALL_G;
+        const dim3 grid((unsigned)((nk + b.G - 1) / b.G * rows));
         if (fi.depth > 8)
             hipLaunchKernelGGL(stall_kernel<2>, grid, dim3(kRowLanes), 0, st, b);
         else

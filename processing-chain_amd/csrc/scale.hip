@@ -664,6 +664,22 @@ void fast_coefs(HostPlane &hp, int dw, int HW) {
     }
 }
 
+// strip_kernel packs an H row pair with v_cvt_pk_i16_i32, whose saturation
+// stands in for hScale*To15's FFMIN(val >> sh, 32767): exact only if no output
+// can fall below -32768 (the most negative sum: every negative tap on a
+// full-scale sample).  Plans that could are left to scale_kernel.
+bool strip_h_sat_ok(const HostPlane &hp, int depth) {
+    const int64_t maxs = (1 << depth) - 1;
+    const int sh = depth == 8 ? 7 : depth - 1;
+    const int taps = hp.h.taps, n = (int)hp.h.pos.size();
+    for (int x = 0; x < n; ++x) {
+        int64_t neg = 0;
+        for (int k = 0; k < taps; ++k) neg += std::min<int64_t>(0, hp.h.coef[(size_t)x * taps + k]);
+        if ((neg * maxs) >> sh < -32768) return false;
+    }
+    return true;
+}
+
 inline int hw_bucket(int need) {
     static const int b[] = {3, 4, 5, 6, 8, 10, 12, 16};
     for (int v : b)
@@ -765,7 +781,7 @@ static int plan_create(pp_ctx *ctx, int src_fmt, int sw, int sh, int dst_fmt, in
         const char *etw = PP_KNOB("PIXPATH_STRIP_TW");
         bool ok0 = !force_generic;
         const int CH = si.depth > 8 ? 8 : 16;
-        for (int c = 0; c < 2 && ok0; ++c) ok0 = hp[c].tw == kTileW && hp[c].vtp <= 8;
+        for (int c = 0; c < 2 && ok0; ++c) ok0 = hp[c].tw == kTileW && hp[c].vtp <= 8 && strip_h_sat_ok(hp[c], si.depth);
         const int tw_first = (etw && atoi(etw) == 512 && !one_seg_chroma && !di.packed) ? 512 : 256;
         for (int ftw = tw_first; ok0 && ftw >= 256; ftw /= 2) {
             bool ok = true;

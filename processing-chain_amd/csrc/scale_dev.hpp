@@ -141,6 +141,15 @@ __device__ inline int dot2_acc(v2i16 a, v2i16 b, int c) {
     return r;
 }
 
+// c + a.lo*b.lo + a.hi*b.hi with b a wave-uniform SGPR and the accumulator c
+// a separate VGPR (VOP3P form): the compiler's v_dot2c form would first copy c
+// into the destination, one v_mov per output
+__device__ inline int dot2_sv(v2i16 a, int32_t b_s, int c) {
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "s"(b_s), "v"(a), "v"(c));
+    return r;
+}
+
 // a.lo*b.lo + a.hi*b.hi with a zero accumulator as an inline constant (the
 // compiler otherwise zeroes a register for the v_dot2c form)
 __device__ inline int dot2_first(v2i16 a, v2i16 b) {

@@ -99,6 +99,25 @@ __device__ inline void store4(uint8_t *drow, int xo, const int o[4], bool vec, i
     }
 }
 
+// clamp(acc >> SH, 0, MX) of two 32-bit V-pass sums, packed as two 16-bit
+// samples (a low, b high): the high halves of both sums in one v_perm, then
+// v_pk_ashrrev_i16 / v_pk_max_i16 / v_pk_min_i16 -- 4 VALU per pair instead
+// of 2 shifts, 2 v_med3 and a v_lshl_or.  Exact: acc >> 16 is the sum's exact
+// signed high half, and (acc >> 16) >> (SH - 16) == acc >> SH.
+// (not in the product: it pushes the config-2 instance to 2 spilled VGPRs)
+#ifndef PIXPATH_PACKED_CLAMP
+#define PIXPATH_PACKED_CLAMP 0
+#endif
+template <int SH, int MX>
+__device__ inline uint32_t clamp_pack16(int a, int b) {
+    static_assert(SH >= 16 && SH < 32 && MX < 32768, "packed clamp range");
+    v2i16 x = __builtin_bit_cast(v2i16, __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x07060302u));
+    if constexpr (SH > 16) x = x >> (v2i16){(short)(SH - 16), (short)(SH - 16)};
+    x = __builtin_elementwise_max(x, (v2i16){0, 0});
+    x = __builtin_elementwise_min(x, (v2i16){(short)MX, (short)MX});
+    return __builtin_bit_cast(uint32_t, x);
+}
+
 // FUSE == 1 (GENERIC_UYVY plans: scale straight into uyvy422, swscale's
 // yuv2packedX with its flat 1 << 18 rounding): every plane stores its 8-bit
 // samples into the one packed row, byte J.pk_off + x * J.pk_step (Y: 1, 2;
@@ -269,6 +288,37 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
         }
     };
 
+    // the same without the clamp: a row pair's results are packed by
+    // v_cvt_pk_i16_i32, whose saturation is the clamp (the host admits a plan
+    // to this kernel only if no output can fall below -32768, strip_h_sat_ok)
+    auto hrow4_raw = [&](const uint16_t *row, int out[4]) {
+        const uint16_t *sp = row + hb;
+        uint32_t w[HW];
+#pragma unroll
+        for (int d = 0; d + 1 < HW; d += 2) {
+            const uint2 v = *reinterpret_cast<const uint2 *>(sp + 2 * d);
+            w[d] = v.x;
+            w[d + 1] = v.y;
+        }
+        if constexpr (HW & 1) w[HW - 1] = *reinterpret_cast<const uint32_t *>(sp + 2 * (HW - 1));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            int acc = dot2_first(__builtin_bit_cast(v2i16, w[0]), hc[j][0]);
+#pragma unroll
+            for (int d = 1; d < HW; ++d) acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, w[d]), hc[j][d], acc, false);
+            out[j] = acc >> hshift;
+        }
+    };
+    // rows a (low halves) and b (high halves) of 4 columns, each clamped to 32767
+    auto pack_pair = [](const int oa[4], const int ob[4]) {
+        uint4 v;
+        v.x = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(oa[0], ob[0]));
+        v.y = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(oa[1], ob[1]));
+        v.z = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(oa[2], ob[2]));
+        v.w = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(oa[3], ob[3]));
+        return v;
+    };
+
     int y_begin = seg * J.seg_h, y_end = min(J.dh, y_begin + J.seg_h);
     int r2lo = 0, r2hi = 0;  // fuse 2: the second-stage rows this segment stores
     if constexpr (FUSE >= 8 && FUSE != 9) {
@@ -315,6 +365,11 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
     const int jfuse = FUSE == 9 ? 1 : FUSE == 11 ? 2 : FUSE >= 8 ? J.fuse : 0;
     constexpr int OUT2 = FUSE == 9 || FUSE == 11 ? 10 : FUSE;  // the chain's output bits
     const kconst int32_t *vrow = as_kconst<int32_t>(J.vrow16);
+    // the V pass's rounding constant in a VGPR: the first v_dot2 of an output
+    // takes it as its accumulator operand (dot2_sv; a literal accumulator cost
+    // a v_mov per output and row)
+    int kround = 1 << (10 + 16 - OUTB);
+    asm volatile("" : "+v"(kround));
     for (int y0 = y_begin; y0 < y_end; y0 += cho) {
         const int ci = y0 / cho;
         const int lo = chunk_lo[ci], hi = chunk_hi[ci];
@@ -376,33 +431,28 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
 #pragma unroll
                     for (int d = 1; d < HW; ++d)
                         acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, w[d]), hc[j][d], acc, false);
-                    acc >>= hshift;
-                    out[j] = acc < 32767 ? acc : 32767;
+                    out[j] = acc >> hshift;  // clamped by the caller (pack_pair or min)
                 }
             };
             auto pair_out = [&](int k, const Win &ra, const Win &rb) {
                 int oa[4], ob[4];
                 hregs(ra, oa);
                 hregs(rb, ob);
-                uint4 v;
-                v.x = __builtin_amdgcn_perm(ob[0], oa[0], 0x05040100u);
-                v.y = __builtin_amdgcn_perm(ob[1], oa[1], 0x05040100u);
-                v.z = __builtin_amdgcn_perm(ob[2], oa[2], 0x05040100u);
-                v.w = __builtin_amdgcn_perm(ob[3], oa[3], 0x05040100u);
-                *reinterpret_cast<uint4 *>(win + k * TW + cx) = v;
+                *reinterpret_cast<uint4 *>(win + k * TW + cx) = pack_pair(oa, ob);
             };
             if ((i0 & 1) && rg == ((i0 >> 1) & 3)) {  // high row of a kept pair
                 int o[4];
                 hregs(ld(i0), o);
                 uint16_t *w16 = reinterpret_cast<uint16_t *>(win + (i0 >> 1) * TW + cx);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) w16[2 * j + 1] = static_cast<uint16_t>(o[j]);
+                for (int j = 0; j < 4; ++j) w16[2 * j + 1] = static_cast<uint16_t>(min(o[j], 32767));
             }
             if (((i0 + nnew) & 1) && rg == (kf1 & 3)) {  // low row of the last pair
                 int o[4];
                 hregs(ld(i0 + nnew - 1), o);
                 uint4 v;
-                v.x = o[0] & 0xffff; v.y = o[1] & 0xffff; v.z = o[2] & 0xffff; v.w = o[3] & 0xffff;
+                v.x = min(o[0], 32767) & 0xffff; v.y = min(o[1], 32767) & 0xffff;
+                v.z = min(o[2], 32767) & 0xffff; v.w = min(o[3], 32767) & 0xffff;
                 *reinterpret_cast<uint4 *>(win + kf1 * TW + cx) = v;
             }
             int k = kf0 + rg;
@@ -434,14 +484,9 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
             for (int k = kf0 + rg; k < kf1; k += 4) {
                 const int ra = 2 * k - i0;
                 int oa[4], ob[4];
-                hrow4(src_t + ra * S, oa);
-                hrow4(src_t + (ra + 1) * S, ob);
-                uint4 v;
-                v.x = __builtin_amdgcn_perm(ob[0], oa[0], 0x05040100u);
-                v.y = __builtin_amdgcn_perm(ob[1], oa[1], 0x05040100u);
-                v.z = __builtin_amdgcn_perm(ob[2], oa[2], 0x05040100u);
-                v.w = __builtin_amdgcn_perm(ob[3], oa[3], 0x05040100u);
-                *reinterpret_cast<uint4 *>(win + k * TW + cx) = v;
+                hrow4_raw(src_t + ra * S, oa);
+                hrow4_raw(src_t + (ra + 1) * S, ob);
+                *reinterpret_cast<uint4 *>(win + k * TW + cx) = pack_pair(oa, ob);
             }
             next_src = hi;
         }
@@ -497,10 +542,18 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
                         for (int j = 0; j < 4; ++j) acc[j] = (int)((d4 >> (8 * j)) & 0xffu) << 12;
                     } else {
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) acc[j] = 1 << (10 + 16 - OUTB);
+                        for (int j = 0; j < 4; ++j) acc[j] = kround;
+                    }
+                    int j0 = 0;
+                    if constexpr (OUTB != 8) {  // first tap pair onto the rounding constant
+                        acc[0] = dot2_sv(__builtin_bit_cast(v2i16, q[0].x), cf[i][0], kround);
+                        acc[1] = dot2_sv(__builtin_bit_cast(v2i16, q[0].y), cf[i][0], kround);
+                        acc[2] = dot2_sv(__builtin_bit_cast(v2i16, q[0].z), cf[i][0], kround);
+                        acc[3] = dot2_sv(__builtin_bit_cast(v2i16, q[0].w), cf[i][0], kround);
+                        j0 = 1;
                     }
 #pragma unroll
-                    for (int j = 0; j < VT; ++j) {
+                    for (int j = j0; j < VT; ++j) {
                         const v2i16 c2 = __builtin_bit_cast(v2i16, cf[i][j]);
                         acc[0] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].x), c2, acc[0], false);
                         acc[1] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].y), c2, acc[1], false);
@@ -510,6 +563,16 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
                     if ((!CL && !lane_any) || (PP_ABLATE(a.debug) & 1)) continue;
                     constexpr int sh = OUTB == 8 ? 19 : 11 + 16 - OUTB;
                     constexpr int mx = (1 << OUTB) - 1;
+                    if constexpr (FUSE == 0 && OUTB > 8 && PIXPATH_PACKED_CLAMP) {
+                        if (CL || (lane_full && a.vec_dst)) {  // 16-bit samples, vector store: packed clamp
+                            uint2 v;
+                            v.x = clamp_pack16<sh, mx>(acc[0], acc[1]);
+                            v.y = clamp_pack16<sh, mx>(acc[2], acc[3]);
+                            *reinterpret_cast<uint2 *>(drow_p + 2 * vxo) = v;
+                            __builtin_amdgcn_sched_barrier(0);
+                            continue;
+                        }
+                    }
                     int o[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) o[j] = min(max(acc[j] >> sh, 0), mx);

@@ -25,7 +25,7 @@ EXPORTS = (
     "pp_ffv1_encoder_create", "pp_ffv1_encoder_destroy", "pp_ffv1_extradata", "pp_ffv1_encode",
     "pp_ffv1_encode_packets", "pp_ffv1_encode_stats", "pp_ffv1_encoder_memory", "pp_ffv1_encoder_reserve",
     "pp_ffv1_decoder_create", "pp_ffv1_decoder_destroy", "pp_ffv1_decoder_format", "pp_ffv1_decoder_slices", "pp_ffv1_decode",
-    "pp_ffv1_decoder_geometry", "pp_ffv1_decoder_info", "pp_ffv1_decoder_reset",
+    "pp_ffv1_decoder_geometry", "pp_ffv1_decoder_info", "pp_ffv1_decoder_reset", "pp_ffv1_decode_group",
 )
 PP_COPY_H2D, PP_COPY_D2H, PP_COPY_D2D = 1, 2, 3
 PP_NAL_H264, PP_NAL_H265 = 1, 2
@@ -117,6 +117,7 @@ def lib():
         "pp_ffv1_decoder_geometry": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "pp_ffv1_decoder_info": (i32, [vp, vp, i32]),
         "pp_ffv1_decoder_reset": (i32, [vp]),
+        "pp_ffv1_decode_group": (i32, [vp, i32, vp, vp, vp, fr, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -136,9 +136,12 @@ class Ffv1Encoder:
             ev.record(stream)
             evs.append(ev)
         host = self._host.numpy()
-        for (a, b, lo, hi), ev in zip(parts, evs):
-            ev.synchronize()
-            yield host[lo:hi], sizes[a:b]
+        try:
+            for (a, b, lo, hi), ev in zip(parts, evs):
+                ev.synchronize()
+                yield host[lo:hi], sizes[a:b]
+        finally:  # a walk abandoned by a failed write leaves no copy in flight into _host
+            stream.synchronize()
 
     def encode_host(self, src, stream=None):
         """(numpy uint8 view of the packets in a pinned host buffer, frame sizes):
@@ -302,6 +305,41 @@ class Ffv1Decoder:
         return dst
 
 
+def decode_group(decoders, packets, sizes, dst=None, stream=None):
+    """One GPU launch over several streams of one configuration record
+    (pp_ffv1_decode_group): decoders[k] decodes packets[k] (frame packets back
+    to back in host memory, sizes[k] each) and keeps its own carried GOP
+    states.  Returns the device FrameBatch of all streams' frames, stream k's
+    at [sum(len(sizes[:k])), ...).  An FFmpeg-made AVPVS (GOP 12, 2x2 slices)
+    has 200 slice chains per 600 frames, one GPU lane each, so one stream
+    alone leaves the GPU almost idle; several side by side fill it."""
+    from .frames import FrameBatch
+    n = len(decoders)
+    if n == 0 or len(packets) != n or len(sizes) != n:
+        raise ValueError("decode_group: one packet buffer and size list per decoder")
+    d0 = decoders[0]
+    datas = []
+    for pk in packets:
+        if isinstance(pk, np.ndarray):
+            datas.append(np.ascontiguousarray(pk, dtype=np.uint8))
+        else:
+            datas.append(np.frombuffer(bytes(pk) if not isinstance(pk, (bytes, bytearray)) else pk, np.uint8))
+    szs = [np.ascontiguousarray(s_, dtype=np.int64) for s_ in sizes]
+    counts = [len(s_) for s_ in szs]
+    total = sum(counts)
+    if dst is None:
+        dst = FrameBatch(d0.fmt, d0.w, d0.h, total, device=torch.device("cuda", d0.ctx.device))
+    elif dst.n < total:
+        raise ValueError("decode_group: dst holds %d frames, the streams %d" % (dst.n, total))
+    handles = (ctypes.c_void_p * n)(*[d.handle.value for d in decoders])
+    pptr = (ctypes.c_void_p * n)(*[d_.ctypes.data for d_ in datas])
+    sptr = (ctypes.c_void_p * n)(*[s_.ctypes.data for s_ in szs])
+    nfr = (ctypes.c_int * n)(*counts)
+    s = dst.frames_struct()
+    check(lib().pp_ffv1_decode_group(handles, n, pptr, sptr, nfr, ctypes.byref(s), _stream(dst.planes[0], stream)))
+    return dst
+
+
 _DEV_LOCK = threading.Lock()
 _DEV_STATE = {}  # device index -> (encode lock, encode stream, host-upload stream, packet D2H stream)
 
@@ -437,6 +475,14 @@ class Ffv1AviWriter:
                     self.stats["timeline"].append((t_q, t_w, t0, t1, t2))
             except Exception as e:  # surfaced by the next write / close
                 self.err.append(e)
+                # a failed AVI write abandons packets_to_host_chunks with later
+                # chunks' D2H copies still queued into the pinned buffer: drain
+                # them before the encoder (and that buffer) can be released or
+                # reused
+                try:
+                    self.d2h_stream.synchronize()
+                except Exception:
+                    pass
             finally:
                 self.free[slot].set()
 
@@ -532,8 +578,9 @@ class Ffv1AviWriter:
         finally:
             if not ok:
                 self.avi.abort()
-                try:  # copies into the staging batch still queued on the caller's stream
-                    self.last_stream.synchronize()
+                try:  # copies into the staging batch still queued on the caller's stream,
+                    self.last_stream.synchronize()  # packet D2H copies on the D2H stream
+                    self.d2h_stream.synchronize()
                 except Exception:
                     pass
             self.release(ok)
@@ -693,16 +740,51 @@ def gpu_decodable(info):
     return True
 
 
+def decoder_route(info, have_ffmpeg=None):
+    """Which decoder reads an AVI's video stream (avi.scan info): "gpu" or
+    "ffmpeg".
+
+    - pixpath's own intra FFV1 (and any intra record the GPU decoder reads):
+      the GPU -- frames x slices chains (38,400 per 600 frames at 8x8).
+    - An FFmpeg-made FFV1 with GOPs (the reference's own AVPVS,
+      `-threads 4 -level 3 -coder 1 -context 1`, lib/ffmpeg.py:993, :1047):
+      one stream has 200 serial chains per 600 frames, one GPU lane each, and
+      decodes slower on the GPU than on the host's cores (bench
+      `reference_stream_decode`), so ffmpeg's decoder takes it when ffmpeg
+      exists; the GPU otherwise.  Several such streams decoded together
+      (decode_group) do fill the GPU.  Parity of the GPU path on FFmpeg's own
+      files is unpinned (no FFmpeg-made FFV1 file exists here; the general
+      decoder is checked against oracle/ffv1_oracle.c's general restatement).
+    - PIXPATH_FFV1_DECODE=gpu|ffmpeg forces one for every stream the GPU
+      decoder reads; PIXPATH_FFV1=ffmpeg (ffmpeg's FFV1 encoder in the gpu
+      backend) also sends records not written by pixpath to ffmpeg.
+    - Anything the GPU decoder refuses: ffmpeg."""
+    import shutil
+    if not gpu_decodable(info):
+        return "ffmpeg"
+    force = os.environ.get("PIXPATH_FFV1_DECODE", "").lower()
+    if force in ("gpu", "ffmpeg"):
+        return force
+    own = is_pixpath_ffv1(info)
+    if not own and os.environ.get("PIXPATH_FFV1", "").lower() == "ffmpeg":
+        return "ffmpeg"
+    if own:
+        return "gpu"
+    dec = Ffv1Decoder(info["extradata"], info["w"], info["h"], max_frames=1, host_only=True)
+    if dec.info.get("intra"):
+        return "gpu"
+    if have_ffmpeg is None:
+        have_ffmpeg = shutil.which("ffmpeg") is not None
+    return "ffmpeg" if have_ffmpeg else "gpu"
+
+
 def open_avpvs_reader(path, device=None, batch=600):
-    """The reader of an AVPVS: the GPU FFV1 decoder (Ffv1AviReader) for an
-    FFV1 AVI it reads -- pixpath's, or the reference's own ffmpeg-made AVPVS --
-    else ffmpeg's decoder through pixpath.io (another codec, or a record the
-    GPU decoder refuses)."""
+    """The reader of an AVPVS: the GPU FFV1 decoder (Ffv1AviReader) or
+    ffmpeg's decoder through pixpath.io, as decoder_route decides."""
     from . import avi, io as pio
-    scanned = None
     if path.lower().endswith(".avi") and os.path.isfile(path):
         scanned = avi.scan(path)
-        if gpu_decodable(scanned[0]):
+        if decoder_route(scanned[0]) == "gpu":
             return Ffv1AviReader(path, batch=batch, device=device, scanned=scanned)
     return pio.open_reader(path)
 

@@ -258,3 +258,36 @@ def test_codec_provenance_in_the_p03_log_line(monkeypatch):
     monkeypatch.setenv("PIXPATH_FFV1", "ffmpeg")
     line = p03_log_line(pff._collapse(pff._gpu_cli("avpvs", args)), "/db/videoSegments", "/db/srcVid")
     assert "--gpu-ffv1" not in line and "-coder 1 -context 1 -slicecrc 1" in line
+
+
+def test_decoder_route_by_stream_shape(monkeypatch):
+    """decoder_route (open_avpvs_reader's choice, VERDICT r5 item 3 / ADVICE r5):
+    pixpath's intra FFV1 goes to the GPU; an FFmpeg-made GOP stream (the
+    reference's AVPVS: 200 serial chains per 600 frames, slower on the GPU
+    than on the host) goes to ffmpeg when ffmpeg exists, else to the GPU;
+    PIXPATH_FFV1_DECODE forces either; PIXPATH_FFV1=ffmpeg sends records not
+    written by pixpath to ffmpeg; a record the GPU decoder refuses goes to
+    ffmpeg."""
+    import ffv1_ref as ref
+    from pixpath import ffv1
+    monkeypatch.delenv("PIXPATH_FFV1_DECODE", raising=False)
+    monkeypatch.delenv("PIXPATH_FFV1", raising=False)
+    base = {"fourcc": b"FFV1", "w": 640, "h": 360}
+    own = dict(base, extradata=ffv1.Ffv1Encoder("yuv422p10le", 640, 360, slices=(8, 8), host_only=True).extradata)
+    gops = dict(base, extradata=ref.gen_extradata(ref.make_prof(10, 1, 0, 2, 2, ref.ffmpeg_context1_sets(10),
+                                                                tidx=(1, 1), coder=2, gop=12)))
+    bad = dict(base, extradata=gops["extradata"][:-1] + b"\0")
+    for have in (True, False):
+        assert ffv1.decoder_route(own, have_ffmpeg=have) == "gpu"
+        assert ffv1.decoder_route(bad, have_ffmpeg=have) == "ffmpeg"
+    assert ffv1.decoder_route(gops, have_ffmpeg=True) == "ffmpeg"
+    assert ffv1.decoder_route(gops, have_ffmpeg=False) == "gpu"
+    monkeypatch.setenv("PIXPATH_FFV1_DECODE", "gpu")
+    assert ffv1.decoder_route(gops, have_ffmpeg=True) == "gpu"
+    assert ffv1.decoder_route(bad, have_ffmpeg=True) == "ffmpeg"
+    monkeypatch.setenv("PIXPATH_FFV1_DECODE", "ffmpeg")
+    assert ffv1.decoder_route(own, have_ffmpeg=False) == "ffmpeg"
+    monkeypatch.delenv("PIXPATH_FFV1_DECODE")
+    monkeypatch.setenv("PIXPATH_FFV1", "ffmpeg")
+    assert ffv1.decoder_route(gops, have_ffmpeg=False) == "ffmpeg"
+    assert ffv1.decoder_route(own, have_ffmpeg=False) == "gpu"

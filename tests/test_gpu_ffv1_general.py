@@ -174,3 +174,38 @@ def test_threshold_quantiser_streams_take_the_pixpath_path(gpu, bounds, name, fi
     dec = ffv1.Ffv1Decoder(ref.gen_extradata(pf), w, h, max_frames=6, device=gpu)
     assert dec.info["pixpath_tables"] == 1
     _check(dec.decode(b"".join(pkts), [len(p) for p in pkts]).to_numpy(), frames)
+
+
+def test_group_decode_of_several_streams(gpu):
+    """pp_ffv1_decode_group: four streams of one record (FFmpeg's GOP shape,
+    each its own content and GOP phase) decoded in ONE launch, then each
+    continued by a second group call that starts inside a GOP (every stream
+    carries its own states); every frame equals the one-stream decode's
+    input.  A stream whose frame 0 is not a keyframe after reset() fails the
+    group with a message naming it; a record mismatch is refused."""
+    from pixpath import ffv1
+    w, h, fid = 320, 180, po.YUV422P10LE
+    pf = ffmpeg_like(10, 1, 0, gop=12)
+    extra = ref.gen_extradata(pf)
+    seqs = [_sequence(pf, fid, w, h, n, 500 + k) for k, n in enumerate((30, 17, 24, 5))]
+    decs = [ffv1.Ffv1Decoder(extra, w, h, max_frames=30, device=gpu) for _ in seqs]
+    cut = (7, 12, 13, 5)  # first call: frames [0, cut), second: the rest
+    first = ffv1.decode_group(decs, [b"".join(p[:c]) for (_, p), c in zip(seqs, cut)],
+                              [[len(x) for x in p[:c]] for (_, p), c in zip(seqs, cut)]).to_numpy()
+    o = 0
+    for (frames, _), c in zip(seqs, cut):
+        _check(first, frames[:c], first=o)
+        o += c
+    rest = [(f[c:], p[c:]) for (f, p), c in zip(seqs, cut)]
+    second = ffv1.decode_group(decs, [b"".join(p) for _, p in rest], [[len(x) for x in p] for _, p in rest]).to_numpy()
+    o = 0
+    for frames, _ in rest:
+        _check(second, frames, first=o)
+        o += len(frames)
+    decs[2].reset()
+    with pytest.raises(Exception, match="stream 2.*keyframe"):
+        ffv1.decode_group(decs[:3], [b"".join(p[c:]) for (_, p), c in zip(seqs[:3], cut)],
+                          [[len(x) for x in p[c:]] for (_, p), c in zip(seqs[:3], cut)])
+    other = ffv1.Ffv1Decoder(ref.gen_extradata(ffmpeg_like(10, 1, 0, nh=1, nv=1)), w, h, max_frames=30, device=gpu)
+    with pytest.raises(Exception, match="one configuration record"):
+        ffv1.decode_group([decs[0], other], [b"".join(seqs[0][1][:12])] * 2, [[len(x) for x in seqs[0][1][:12]]] * 2)

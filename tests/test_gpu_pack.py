@@ -91,6 +91,35 @@ def test_stall_compose_matches_oracle(gpu, fmt, w, h, dense):
             np.testing.assert_array_equal(out[p][k], ref[p], err_msg="frame %d plane %d" % (k, p))
 
 
+def test_stall_compose_long_runs_across_tiles(gpu):
+    """A stall run as the product composes it (one frozen frame repeated,
+    spinner animating) mixed with source changes and black frames, 300 frames:
+    the kernel's tiles of G frames per wave (one source load, G stores), the
+    256-frame launch split and a source change inside a tile all equal the
+    oracle."""
+    from pixpath import ops, spinner
+    fmt, w, h = po.YUV422P10LE, 320, 180
+    anim, _ = spinner.load_apng(GOLDEN_SPINNER)
+    rng = np.random.default_rng(405)
+    frames = [synth.noise_frame(rng, fmt, w, h) for _ in range(3)]
+    src = _batch(fmt, frames, gpu, False)
+    ops.spinner_upload(anim, fmt)
+    src_idx = np.array([0] * 131 + [1] * 7 + [-1] * 5 + [2, 0, 2, 1] * 39 + [1], np.int32)
+    sp_idx = (np.arange(len(src_idx)) % len(anim)).astype(np.int32)
+    sp_idx[140:150] = -1
+    out = ops.stall_compose(src, src_idx, sp_idx).to_numpy()
+    depth = po.fmt_info(fmt)[0]
+    for k in list(range(0, len(src_idx), 7)) + [130, 131, 137, 138, 142, 143, 255, 256, len(src_idx) - 1]:
+        if src_idx[k] >= 0:
+            base = frames[src_idx[k]]
+        else:
+            base = [np.full(s, (16 if p == 0 else 128) << (depth - 8), dtype=po.plane_dtype(fmt))
+                    for p, s in enumerate(po.plane_shapes(fmt, w, h))]
+        ref = base if sp_idx[k] < 0 else po.overlay_spinner(fmt, base, po.spinner_to_yuva(anim[sp_idx[k]], fmt))
+        for p in range(3):
+            np.testing.assert_array_equal(out[p][k], ref[p], err_msg="frame %d plane %d" % (k, p))
+
+
 @pytest.mark.parametrize("fmt,w,h,W,H", [
     (po.YUV420P, 1920, 800, 1920, 1080), (po.YUV420P, 1920, 1080, 1920, 1080), (po.YUV422P, 1920, 1012, 1920, 1080),
     (po.YUV420P10LE, 1920, 1080, 1920, 1080), (po.YUV420P10LE, 1920, 800, 1920, 1080),

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     assert declared == set(_native.EXPORTS)
     for name in declared:
         assert hasattr(L, name)
-    assert L.pp_abi_version() == 6
+    assert L.pp_abi_version() == 7
 
 
 def test_host_transfer_argument_checks():
