@@ -70,7 +70,7 @@ def frame_bytes(fmt, w, h):
 # records them in the line.  The product library reads no environment at all
 # (csrc/common.hpp PP_KNOB); these guard the Python side and PIXPATH_LIB.
 PRODUCT_ENV = {"PIXPATH_DEVICE", "PIXPATH_SLOT_DIR", "PIXPATH_BACKEND", "PIXPATH_FFV1", "PIXPATH_FFV1_SLICES",
-               "PIXPATH_SPINNER", "PIXPATH_HOME"}
+               "PIXPATH_FFV1_SPLIT", "PIXPATH_FFV1_DECODE", "PIXPATH_SPINNER", "PIXPATH_HOME"}
 
 
 def tuning_overrides():
@@ -269,8 +269,17 @@ def cpu_baseline(args, wl):
     # the best rate this box's host gives the CPU path (the cgroup's CPU quota
     # caps it below the affinity width; more threads than the quota only add
     # contention), with the thread count that reached it; then the other
-    # build at that count: `value` is the faster build's (the box's EPYC ran
-    # the -march=native build slower than the scalar one: 576 vs 760 frames/s)
+    # build at that count: `value` is the faster build's.  The box's EPYC
+    # (Zen 5) runs the -march=native SCALER slower than the scalar build
+    # (576-715 vs 760-1,040 frames/s) while its SI/TI is faster: the native
+    # build vectorises each output's short tap loop of hscale_row (8 taps:
+    # vpmovzxwd + vpmulld, then a horizontal reduction through vextracti128 /
+    # vpsrldq / vpaddd per output -- checked in gcc's x86-64-v4 assembly of
+    # oracle/pixoracle.c), which costs more per output than the scalar
+    # multiply-adds; the Sobel / difference loops are contiguous streams that
+    # vectorise well.  Each stage is timed
+    # at both builds and taken at its faster one, so the baseline is the most
+    # favourable CPU number either build gives.
     top = max(sweep, key=lambda r: r["value"])
     other = point(po, setup(po, top["threads"]), top["threads"], max(2.0, args.cpu_seconds / 2)) if native_path else None
     builds = {ORACLE_SCALAR_FLAGS: top}
@@ -484,7 +493,8 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None, shared=True):
         return [os.path.join(d, "r%d_PVS%d.avi" % (runs[0], k)) for k in range(count)]
     depth = depth or n_pvs  # every PVS of the run can be in flight at once
     t_res = time.perf_counter()
-    made = ffv1.reserve_encoders(dfmt, dw, dh, depth, slices=(8, 8), max_frames=n_frames, device=dev.index)
+    split = ffv1.default_split()
+    made = ffv1.reserve_writers(dfmt, dw, dh, depth, slices=(8, 8), batch=n_frames, device=dev.index, split=split)
     torch.cuda.synchronize()
     reserve_s = time.perf_counter() - t_res
 
@@ -525,12 +535,16 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None, shared=True):
         dt = t_end - t0
         order = sorted(stats, key=lambda w: w["timeline"][0][0] if w["timeline"] else 0)
         st = {"setup_s": setup_s, "pipeline_s": pipe_s, "tail_s": round(t_end - t_main, 4),
-              # per PVS, seconds from the run's start: batch queued, frames ready on the
-              # GPU (encode starts), encode done (packet D2H starts), packets written
-              # (D2H chunks overlapped with the writes), AVI closed
+              # per PVS, seconds from the run's start: first (sub-)batch queued, its
+              # frames ready on the GPU (encode starts), the last encode done, the
+              # last packets written (D2H chunks overlapped with the writes), AVI
+              # closed; lanes: each sub-batch's (queued, encode start, encode done,
+              # written)
               "timeline": [[round(x - t0, 4) for x in (w["timeline"][0][0], w["timeline"][0][2],
-                                                       w["timeline"][0][3], w["timeline"][0][4], w["closed_at"])]
+                                                       max(t[3] for t in w["timeline"]),
+                                                       max(t[4] for t in w["timeline"]), w["closed_at"])]
                            for w in order if w["timeline"]],
+              "lanes": [[[round(t[i] - t0, 4) for i in (0, 2, 3, 4)] for t in w["timeline"]] for w in order],
               "encode_s": [round(w["encode_s"], 4) for w in order],
               "d2h_and_avi_write_s": [round(w["write_s"], 4) for w in order],
               "encode_launches": [w["launches"] for w in order]}
@@ -555,8 +569,8 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None, shared=True):
         os.rmdir(d)
     enc_mem = None
     try:
-        e = ffv1.acquire_encoder(dfmt, dw, dh, slices=(8, 8), max_frames=n_frames, device=dev.index)
-        enc_mem = e.memory_bytes + sum(b.storage.numel() for b in (e.stages or []))
+        e = ffv1.acquire_encoder(dfmt, dw, dh, slices=(8, 8), max_frames=-(-n_frames // split), device=dev.index)
+        enc_mem = split * (e.memory_bytes + sum(b.storage.numel() for b in (e.stages or [])))
         ffv1.release_encoder(e)
     except Exception:
         pass
@@ -564,13 +578,15 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None, shared=True):
     return {"frames_per_s": round(n / dt, 1), "frames": n, "pvs": n_pvs, "seconds": round(dt, 3), "stages": ws,
             "single_pvs": {"frames_per_s": round(n1 / dt1, 1), "seconds": round(dt1, 3), "runs_s": single_runs,
                            "stages": w1},
-            "writers": "one encode stream and lock per device" if shared else "own streams, concurrent encodes",
+            "writers": ("%d encoder lanes per writer (sub-batches of %d frames coded side by side, packets written "
+                        "in frame order; PIXPATH_FFV1_SPLIT)" % (split, -(-n_frames // split)) if split > 1 else
+                        "one encode stream and lock per device" if shared else "own streams, concurrent encodes"),
             "encoder_pool": {"depth": depth, "created": made, "reserve_s": round(reserve_s, 3),
                              "bytes_per_writer": enc_mem},
             "avi_bytes_per_pvs": size, "compression": round(n1 * frame_bytes(dfmt, dw, dh) / size, 3),
             "note": "%d PVSes of %d frames: host frames -> pinned batches of 60 -> H2D -> strip_kernel "
-                    "(720p->1080p yuv422p10le lanczos) -> FFV1 v3 encode on the device output (8x8 slices, one "
-                    "batch per PVS, the writer's worker thread and stream) -> packets D2H -> AVI file; consecutive "
+                    "(720p->1080p yuv422p10le lanczos) -> FFV1 v3 encode on the device output (8x8 slices, the "
+                    "writer's encoder lanes: worker threads and streams) -> packets D2H -> AVI file; consecutive "
                     "PVSes overlap; %d pooled encoders reserved before timing; decode of the SRC bitstream "
                     "excluded (ffmpeg is absent on the box)" % (n_pvs, n_frames, depth)}
 
@@ -732,6 +748,10 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_source": ("copied from profiles/pmc_traffic.json: HBM bytes per launch of separate rocprofv3 "
+                               "--pmc FETCH_SIZE / WRITE_SIZE passes of this workload (tools/pmc_traffic.py, "
+                               "read side doubled per MI355X_MICROARCH.md), not measured in this run"
+                               if traffic is not None else None),
             "algorithmic_bytes_per_launch": bytes_pf * n,
             "avg_launch_ms": round(scale_ms, 4),
             "plan": dict(scaler.stats, kernel_path=scaler.kernel_path),
@@ -800,6 +820,23 @@ def bench_stall(args, rank, world, dev):
     # is read once per launch), against the measured store ceiling of the box
     # (contiguous dwordx4 stores, profiles/r2/strip_experiments.md: 6,774 GB/s)
     write_gbs = fb * n / (ms / 1000.0) / 1e9
+    # PMC traffic of the stall launches, copied from the committed profile of
+    # this workload (tools/gpu_final_r6.sh: separate --pmc FETCH_SIZE /
+    # WRITE_SIZE passes, tools/pmc_traffic.py), scaled from its per-launch
+    # mean (<= 256 frames a launch) to this line's frames
+    stall_traffic = None
+    try:
+        pm = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic_config4.json")))
+        k = pm["kernels"].get("stall_kernel")
+        if k and pm.get("frames_per_launch") == n:
+            nl = (n + 255) // 256
+            stall_traffic = {"hbm_bytes": round(k["hbm_bytes_per_launch"] * nl),
+                             "read_bytes": round(k["read_bytes_corrected"] * nl),
+                             "write_bytes": round(k["write_bytes"] * nl),
+                             "source": "copied from profiles/pmc_traffic_config4.json (separate rocprofv3 --pmc "
+                                       "passes of this workload), not measured in this run"}
+    except (OSError, ValueError, KeyError):
+        stall_traffic = None
     # the long test's canvases (create_avpvs_segment): 720p yuv420p10le segment
     # frames -> overlay yuv420p -> yuv422p10le 1080p, one chain-plan launch
     seg = FrameBatch("yuv420p10le", 1280, 720, n, device=dev)
@@ -833,7 +870,8 @@ def bench_stall(args, rank, world, dev):
                           "config": {"workload": DESCR["config4"], "frames_per_launch": n},
                           "roofline": {"bound": "hbm", "kernel": "stall_kernel", "achieved": round(achieved, 1),
                                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                                       "traffic": None, "algorithmic_bytes_per_launch": 2 * fb * n,
+                                       "traffic": stall_traffic["hbm_bytes"] if stall_traffic else None,
+                                       "traffic_detail": stall_traffic, "algorithmic_bytes_per_launch": 2 * fb * n,
                                        "avg_launch_ms": round(ms, 4),
                                        "note": "SURVEY 8d bytes (read + write per frame); the frozen frame is "
                                                "read from HBM once per launch, so write_gbs is the HBM figure"},
@@ -934,6 +972,48 @@ def bench_ffv1(args, rank, world, dev):
                 "decode_frames_per_s": round(world * K * n / ddt_c, 1), "lossless": ok,
                 "note": "%d 600-frame batches at once (own encoder/decoder, stream and host thread each); "
                         "best of %d" % (K, max(1, args.steps))}
+    # the AVPVS writer's encoder lanes (PIXPATH_FFV1_SPLIT): the same batch as
+    # K sub-batches on K encoders, streams and host threads at once
+    lanes = None
+    K = ffv1.default_split()
+    if K > 1 and n % K == 0:
+        import threading
+        sub = n // K
+        lencs = [ffv1.Ffv1Encoder("yuv422p10le", w, h, slices=(nh, nv), max_frames=sub, device=dev) for _ in range(K)]
+        lstreams = [torch.cuda.Stream(dev) for _ in range(K)]
+        parts = [FrameBatch.interleaved("yuv422p10le", w, h, sub, device=dev) for _ in range(K)]
+        for k in range(K):
+            for p in range(3):
+                parts[k].view(p).copy_(src.view(p)[k * sub:(k + 1) * sub])
+        torch.cuda.synchronize()
+
+        def lanes_once():
+            def one(k):
+                with torch.cuda.stream(lstreams[k]):
+                    lencs[k].encode(parts[k], stream=lstreams[k])
+            ths = [threading.Thread(target=one, args=(k,)) for k in range(K)]
+            t0 = time.perf_counter()
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+            torch.cuda.synchronize()
+            return time.perf_counter() - t0
+        lanes_once()
+        ldt = min(lanes_once() for _ in range(max(1, args.steps)))
+        one_dt = []
+        for _ in range(max(1, args.steps)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            lencs[0].encode(parts[0])
+            torch.cuda.synchronize()
+            one_dt.append(time.perf_counter() - t0)
+        lanes = {"lanes": K, "frames_per_lane": sub, "batch_s": round(ldt, 4),
+                 "frames_per_s": round(world * n / ldt, 1), "one_sub_batch_alone_s": round(min(one_dt), 4),
+                 "note": "the %d-frame batch as %d sub-batches encoded at once (own encoder, stream and host thread "
+                         "each: the AVPVS writer's lanes), best of %d; one_sub_batch_alone_s: one sub-batch with "
+                         "the GPU to itself" % (n, K, max(1, args.steps))}
+        del lencs, parts
     out = {"metric": "FFV1 AVPVS encode frames/s (1080p yuv422p10le)", "value": round(world * n / dt, 1),
            "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -943,7 +1023,7 @@ def bench_ffv1(args, rank, world, dev):
                       "compression": round(raw / float(sizes.mean()), 3)},
            "decode": {"frames_per_s": round(world * n / ddt, 1), "ms_per_step": round(ddt * 1e3, 3),
                       "lossless": lossless, "note": "packets from host memory (H2D included)"},
-           "concurrent": conc,
+           "concurrent": conc, "writer_lanes": lanes,
            "roofline": None, "library": library_id(), "tuning_overrides": tuning_overrides() or None}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -1020,7 +1100,7 @@ def reference_stream_decode(args, src, dev, ffv1_ref):
     decs = []
     for K in (1, 4, 16):
         free = torch.cuda.mem_get_info(dev)[0]
-        if K * m * (fb + len(one) / gop) * 1.2 > 0.5 * free:
+        if K * m * (fb + len(one) / gop) * 1.1 > 0.85 * free:
             rows.append({"streams": K, "skipped": "needs %.1f GB of HBM" % (K * m * fb / 1e9)})
             continue
         while len(decs) < K:

@@ -240,6 +240,15 @@ def reserve_encoders(fmt, w, h, count, slices=(8, 8), max_frames=600, device=Non
     return len(made)
 
 
+def reserve_writers(fmt, w, h, count, slices=(8, 8), batch=600, device=None, split=None):
+    """reserve_encoders for `count` AVPVS writers (Ffv1AviWriter) of `batch`
+    frames with `split` encoder lanes each (default_split()): count x split
+    encoders of ceil(batch / split) frames, one staging batch each."""
+    k = default_split() if split is None else max(1, int(split))
+    sub = -(-int(batch) // k)
+    return reserve_encoders(fmt, w, h, count * k, slices=slices, max_frames=sub, device=device, stages=1)
+
+
 def clear_pool():
     """Free every idle pooled encoder (and its staging batches)."""
     with _POOL_LOCK:
@@ -360,10 +369,41 @@ def _device_state(device):
         return st
 
 
+_SEMS = {}  # (device, lanes) -> semaphore of the encoder lanes' encodes
+
+
+def _lane_semaphore(device, lanes):
+    """At most `lanes` lane encodes at once on a device, over every writer of
+    the process: the K sub-batches of one writer code side by side (K x 1/K of
+    a batch is one batch's worth of slice chains), while the lanes of several
+    writers queue as whole batches did under the shared encode lock
+    (concurrent full-batch encodes measured slower than serial ones, see
+    _device_state)."""
+    with _DEV_LOCK:
+        s = _SEMS.get((device, lanes))
+        if s is None:
+            s = _SEMS[(device, lanes)] = threading.BoundedSemaphore(lanes)
+        return s
+
+
 def provenance(slices):
     """The encoder tag written into the AVPVS (RIFF INFO ISFT) and echoed in
     the GPU command string p03 logs as `ffmpegCommand:` (p03_generateAvPvs.py:41-59)."""
     return "pixpath ffv1-gpu v3 intra %dx%d slices" % (int(slices[0]), int(slices[1]))
+
+
+def default_split():
+    """Encoders per AVPVS writer (PIXPATH_FFV1_SPLIT, default 2): the 600-frame
+    batch of a PVS is coded as that many sub-batches, each on its own encoder,
+    stream and worker thread, so the first half's encode starts while the
+    pipeline still scales the second half, the halves code side by side (one
+    600-frame encode leaves ~40 % of the SIMDs idle: 600 waves for 1,024), and
+    the first half's packets are written to the AVI while the second half
+    codes.  1 restores one encoder and one encode per batch."""
+    v = os.environ.get("PIXPATH_FFV1_SPLIT", "2")
+    if not v.isdigit() or not 1 <= int(v) <= 8:
+        raise ValueError("PIXPATH_FFV1_SPLIT must be 1..8")
+    return int(v)
 
 
 class Ffv1AviWriter:
@@ -374,71 +414,99 @@ class Ffv1AviWriter:
     Frames accumulate in HBM -- straight from the pipeline's device output
     (``write_device``: no D2H, no re-upload) or from host frames (``write``) --
     into batches of ``batch`` frames (default 600, a 10 s PVS at 60 fps: the
-    encoder's parallelism is frames x slices).  A full batch is encoded by a
-    worker thread on its own stream while the next batch fills (a second
-    staging batch, allocated only when a PVS has more than one batch), its
-    packets come back in one pinned D2H and go into the AVI.  The encoder and
-    its staging batches come from the process's pool (acquire_encoder)."""
+    encoder's parallelism is frames x slices).  With ``split`` = 1 a full batch
+    is encoded by a worker thread on its own stream while the next batch fills
+    (a second staging batch, allocated only when a PVS has more than one
+    batch), its packets come back in one pinned D2H and go into the AVI.  With
+    ``split`` = K > 1 (the default, default_split) the batch is K sub-batches
+    on K encoder LANES -- each lane its own encoder, staging batch, streams and
+    worker thread -- submitted as each fills: the lanes' encodes overlap the
+    pipeline and each other, and a lane writes its packets as soon as the
+    lanes before it in frame order have written theirs.  The encoders and
+    their staging batches come from the process's pool (acquire_encoder)."""
 
-    def __init__(self, path, fmt, w, h, rate, slices=None, batch=600, device=None, shared=True):
+    def __init__(self, path, fmt, w, h, rate, slices=None, batch=600, device=None, shared=True, split=None):
         """slices: the FFV1 slice grid (default PIXPATH_FFV1_SLICES, else 8x8;
         16x16 encodes ~1.3x faster at ~7 % larger files).
-        shared: encode on the device's shared stream under its encode lock
-        (_device_state); False gives the writer its own streams and lets its
-        encodes overlap other writers' (bench comparison only)."""
+        shared (split = 1 only): encode on the device's shared stream under
+        its encode lock (_device_state); False gives the writer its own
+        streams and lets its encodes overlap other writers' (bench comparison
+        only).  split: encoder lanes (default_split())."""
         import time
         from . import avi
         t0 = time.perf_counter()
         if slices is None:
             slices = default_slices()
+        if split is None:
+            split = default_split()
         self.fmt = formats.fmt(fmt)
         self.w, self.h = int(w), int(h)
         self.fb = formats.frame_bytes(self.fmt, w, h)
         self.batch = int(batch)
-        self.enc = acquire_encoder(self.fmt, w, h, slices=slices, max_frames=self.batch, device=device)
+        self.K = max(1, min(int(split), self.batch))
+        self.sub = -(-self.batch // self.K)  # frames per sub-batch (lane batch)
+        self.encs = [acquire_encoder(self.fmt, w, h, slices=slices, max_frames=self.sub, device=device)
+                     for _ in range(self.K)]
+        self.enc = self.encs[0]
         self.device = torch.device("cuda", self.enc.ctx.device)
-        if self.enc.stages is None:
-            self.enc.stages = []
+        for e in self.encs:
+            if e.stages is None:
+                e.stages = []
+        # staging slots: split = 1 double-buffers on the one encoder (slots 0, 1),
+        # else one slot per lane; slot s is coded by encoder lane_of[s]
+        self.nslots = 2 if self.K == 1 else self.K
+        self.lane_of = [0, 0] if self.K == 1 else list(range(self.K))
         self._stage(0)
-        self.free = [threading.Event(), threading.Event()]
+        self.free = [threading.Event() for _ in range(self.nslots)]
         for e in self.free:
             e.set()
         self.cur, self.fill = 0, 0
         self.free[0].clear()
-        if shared:
-            self.lock, self.stream, self.put_stream, self.d2h_stream = _device_state(self.device.index)
+        if shared and self.K == 1:
+            lock, st, self.put_stream, d2h = _device_state(self.device.index)
+            self.lanes = [(lock, st, d2h)]
         else:
-            self.lock = threading.Lock()
-            self.stream = torch.cuda.Stream(self.device)
             self.put_stream = torch.cuda.Stream(self.device)  # host-frame uploads
-            self.d2h_stream = torch.cuda.Stream(self.device)  # packet D2H
+            sem = _lane_semaphore(self.device.index, self.K) if shared else threading.BoundedSemaphore(self.K)
+            self.lanes = [(sem, torch.cuda.Stream(self.device), torch.cuda.Stream(self.device))
+                          for _ in range(self.K)]
+        self.stream, self.d2h_stream = self.lanes[0][1], self.lanes[0][2]
         self.avi = avi.AviWriter(path, w, h, rate, extradata=self.enc.extradata,
                                  info={b"ISFT": provenance(self.enc.slices).encode()})
         self.frames = 0
         # worker-thread time per part; setup_s: encoder + staging + file open (0 allocations when pooled)
-        self.stats = {"encode_s": 0.0, "write_s": 0.0, "bytes": 0, "launches": 0,
+        self.stats = {"encode_s": 0.0, "write_s": 0.0, "bytes": 0, "launches": 0, "lanes": self.K,
                       "setup_s": time.perf_counter() - t0, "timeline": []}
         self.last_stream = self.put_stream
-        self.q = queue.Queue()
+        self.seq = 0          # sub-batches submitted
+        self.turn = 0         # the next sub-batch (in frame order) whose packets go into the AVI
+        self.turn_cv = threading.Condition()
         self.err = []
-        self.th = threading.Thread(target=self._work, daemon=True)
-        self.th.start()
+        self.qs = [queue.Queue() for _ in range(self.K)]
+        self.ths = [threading.Thread(target=self._work, args=(k,), daemon=True) for k in range(self.K)]
+        for t in self.ths:
+            t.start()
 
-    def _stage(self, k):
+    def _stage(self, slot):
         from .frames import FrameBatch
-        st = self.enc.stages
+        enc = self.encs[self.lane_of[slot]]
+        k = slot if self.K == 1 else 0
+        st = enc.stages
         while len(st) <= k:
-            st.append(FrameBatch.interleaved(self.fmt, self.w, self.h, self.batch, device=self.device))
+            st.append(FrameBatch.interleaved(self.fmt, self.w, self.h, self.sub, device=self.device))
         return st[k]
 
-    def _work(self):
+    def _work(self, lane):
         import time
         from .frames import FrameBatch
+        enc = self.encs[lane]
+        lock, stream, d2h = self.lanes[lane]
         while True:
-            item = self.q.get()
+            item = self.qs[lane].get()
             if item is None:
                 return
-            slot, n, ev, t_q = item
+            slot, n, ev, t_q, seq = item
+            mine = released = False
             try:
                 if self.err:
                     # after a failure: still wait for this batch's copies into the
@@ -447,32 +515,43 @@ class Ffv1AviWriter:
                     ev.synchronize()
                 else:
                     t_w = time.perf_counter()
-                    self.stream.wait_event(ev)
+                    stream.wait_event(ev)
                     ev.synchronize()  # the frames of this batch are in the staging batch
                     src = FrameBatch.interleaved(self.fmt, self.w, self.h, n, device=self.device,
-                                                 storage=self.enc.stages[slot].storage[:n])
-                    with self.lock:  # the device's encodes one at a time, on its encode stream
+                                                 storage=self._stage(slot).storage[:n])
+                    # split = 1: the device's encodes one at a time, on its encode
+                    # stream; lanes: at most K lane encodes at once on the device
+                    with lock:
                         t0 = time.perf_counter()
-                        with torch.cuda.stream(self.stream):
-                            ptr, n, sizes = self.enc.encode_packets(src, stream=self.stream)
+                        with torch.cuda.stream(stream):
+                            ptr, n, sizes = enc.encode_packets(src, stream=stream)
+                    released = True  # the staging batch is read: the next sub-batch may fill it
+                    self.free[slot].set()
                     # the packets leave on the D2H stream, outside the lock: the next
                     # writer's encode starts while this D2H runs, and no writer's host
                     # upload (put_stream, synchronised per upload) waits behind it
                     # (ADVICE r4); the D2H waits for the encode on its stream
-                    self.d2h_stream.wait_stream(self.stream)
+                    d2h.wait_stream(stream)
                     t1 = time.perf_counter()
-                    # packets D2H in chunks, each written to the AVI as it lands
-                    # (the copy of chunk k + 1 overlaps the write of chunk k)
-                    for data, part in self.enc.packets_to_host_chunks(ptr, n, sizes, self.d2h_stream):
-                        self.avi.write_packets(data, part)
-                    t2 = time.perf_counter()
-                    self.stats["encode_s"] += t1 - t0
-                    self.stats["write_s"] += t2 - t1
-                    self.stats["bytes"] += int(sizes.sum())
-                    self.stats["launches"] += self.enc.launches
-                    # timeline (perf_counter): batch queued, worker picked it up,
-                    # its frames ready on the GPU, packets on the host, packets written
-                    self.stats["timeline"].append((t_q, t_w, t0, t1, t2))
+                    # the AVI takes the sub-batches in frame order
+                    with self.turn_cv:
+                        while self.turn != seq and not self.err:
+                            self.turn_cv.wait()
+                        mine = not self.err
+                    if mine:
+                        t_t = time.perf_counter()
+                        # packets D2H in chunks, each written to the AVI as it lands
+                        # (the copy of chunk k + 1 overlaps the write of chunk k)
+                        for data, part in enc.packets_to_host_chunks(ptr, n, sizes, d2h):
+                            self.avi.write_packets(data, part)
+                        t2 = time.perf_counter()
+                        self.stats["encode_s"] += t1 - t0
+                        self.stats["write_s"] += t2 - t_t
+                        self.stats["bytes"] += int(sizes.sum())
+                        self.stats["launches"] += enc.launches
+                        # timeline (perf_counter): batch queued, worker picked it up,
+                        # its frames ready on the GPU, packets on the host, packets written
+                        self.stats["timeline"].append((t_q, t_w, t0, t1, t2))
             except Exception as e:  # surfaced by the next write / close
                 self.err.append(e)
                 # a failed AVI write abandons packets_to_host_chunks with later
@@ -480,11 +559,16 @@ class Ffv1AviWriter:
                 # them before the encoder (and that buffer) can be released or
                 # reused
                 try:
-                    self.d2h_stream.synchronize()
+                    d2h.synchronize()
                 except Exception:
                     pass
             finally:
-                self.free[slot].set()
+                if not released:  # once per item: the slot may already hold the next sub-batch
+                    self.free[slot].set()
+                with self.turn_cv:
+                    if mine or self.err:
+                        self.turn = max(self.turn, seq + 1)
+                    self.turn_cv.notify_all()
 
     def _check(self):
         if self.err:
@@ -494,8 +578,9 @@ class Ffv1AviWriter:
         import time
         ev = torch.cuda.Event()
         ev.record(stream)
-        self.q.put((self.cur, self.fill, ev, time.perf_counter()))
-        self.cur ^= 1
+        self.qs[self.lane_of[self.cur]].put((self.cur, self.fill, ev, time.perf_counter(), self.seq))
+        self.seq += 1
+        self.cur = (self.cur + 1) % self.nslots
         self.free[self.cur].wait()
         self.free[self.cur].clear()
         self.fill = 0
@@ -505,7 +590,7 @@ class Ffv1AviWriter:
         """Append device frames (uint8 rows [k, frame_bytes]) on `stream`."""
         k, i = rows.shape[0], 0
         while i < k:
-            take = min(k - i, self.batch - self.fill)
+            take = min(k - i, self.sub - self.fill)
             stage = self._stage(self.cur)
             with torch.cuda.stream(stream):
                 stage.storage[self.fill:self.fill + take].copy_(rows[i:i + take], non_blocking=True)
@@ -513,7 +598,7 @@ class Ffv1AviWriter:
             self.frames += take
             i += take
             self.last_stream = stream
-            if self.fill == self.batch:
+            if self.fill == self.sub:
                 self._submit(stream)
         if stream is self.put_stream:  # host uploads complete before any event on another stream
             stream.synchronize()
@@ -551,10 +636,11 @@ class Ffv1AviWriter:
         self._put(d, self.put_stream)
 
     def release(self, ok=True):
-        """After close(): the encoder and its staging batches go back to the
+        """After close(): the encoders and their staging batches go back to the
         pool (freed instead when the encode failed)."""
-        if self.enc is not None:
-            release_encoder(self.enc, ok=ok)
+        for e in self.encs or []:
+            release_encoder(e, ok=ok)
+        self.encs = []
         self.enc = None
 
     def close(self):
@@ -566,10 +652,13 @@ class Ffv1AviWriter:
                 import time
                 ev = torch.cuda.Event()
                 ev.record(self.last_stream)
-                self.q.put((self.cur, self.fill, ev, time.perf_counter()))
+                self.qs[self.lane_of[self.cur]].put((self.cur, self.fill, ev, time.perf_counter(), self.seq))
+                self.seq += 1
                 self.fill = 0
-            self.q.put(None)
-            self.th.join()
+            for q in self.qs:
+                q.put(None)
+            for t in self.ths:
+                t.join()
             self._check()
             self.avi.close()
             ok = True
@@ -579,8 +668,9 @@ class Ffv1AviWriter:
             if not ok:
                 self.avi.abort()
                 try:  # copies into the staging batch still queued on the caller's stream,
-                    self.last_stream.synchronize()  # packet D2H copies on the D2H stream
-                    self.d2h_stream.synchronize()
+                    self.last_stream.synchronize()  # packet D2H copies on the D2H streams
+                    for _, _, d2h in self.lanes:
+                        d2h.synchronize()
                 except Exception:
                     pass
             self.release(ok)
