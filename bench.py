@@ -493,8 +493,11 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None, shared=True):
         return [os.path.join(d, "r%d_PVS%d.avi" % (runs[0], k)) for k in range(count)]
     depth = depth or n_pvs  # every PVS of the run can be in flight at once
     t_res = time.perf_counter()
+    # encoder lanes per writer (writer_split): default_split() for a writer that
+    # codes alone on the device, 1 for writers opened while another is open
     split = ffv1.default_split()
-    made = ffv1.reserve_writers(dfmt, dw, dh, depth, slices=(8, 8), batch=n_frames, device=dev.index, split=split)
+    forced = bool(os.environ.get("PIXPATH_FFV1_SPLIT"))
+    made = ffv1.reserve_writers(dfmt, dw, dh, depth, slices=(8, 8), batch=n_frames, device=dev.index)
     torch.cuda.synchronize()
     reserve_s = time.perf_counter() - t_res
 
@@ -547,7 +550,8 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None, shared=True):
               "lanes": [[[round(t[i] - t0, 4) for i in (0, 2, 3, 4)] for t in w["timeline"]] for w in order],
               "encode_s": [round(w["encode_s"], 4) for w in order],
               "d2h_and_avi_write_s": [round(w["write_s"], 4) for w in order],
-              "encode_launches": [w["launches"] for w in order]}
+              "encode_launches": [w["launches"] for w in order],
+              "writer_lanes": [w["lanes"] for w in order]}
         # the main thread's stages plus the wait for the last writers: the wall time
         st["explained_s"] = round(sum(setup_s) + sum(pipe_s) + st["tail_s"], 4)
         st["explained_frac"] = round(st["explained_s"] / dt, 4)
@@ -567,20 +571,24 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None, shared=True):
         for f in os.listdir(d):
             os.remove(os.path.join(d, f))
         os.rmdir(d)
-    enc_mem = None
-    try:
-        e = ffv1.acquire_encoder(dfmt, dw, dh, slices=(8, 8), max_frames=-(-n_frames // split), device=dev.index)
-        enc_mem = split * (e.memory_bytes + sum(b.storage.numel() for b in (e.stages or [])))
-        ffv1.release_encoder(e)
-    except Exception:
-        pass
+    enc_mem = {}
+    for k in sorted({split, 1}):
+        try:
+            e = ffv1.acquire_encoder(dfmt, dw, dh, slices=(8, 8), max_frames=-(-n_frames // k), device=dev.index)
+            enc_mem["%d_lanes" % k] = k * (e.memory_bytes + sum(b.storage.numel() for b in (e.stages or [])))
+            ffv1.release_encoder(e)
+        except Exception:
+            pass
     ffv1.clear_pool()
     return {"frames_per_s": round(n / dt, 1), "frames": n, "pvs": n_pvs, "seconds": round(dt, 3), "stages": ws,
             "single_pvs": {"frames_per_s": round(n1 / dt1, 1), "seconds": round(dt1, 3), "runs_s": single_runs,
                            "stages": w1},
             "writers": ("%d encoder lanes per writer (sub-batches of %d frames coded side by side, packets written "
-                        "in frame order; PIXPATH_FFV1_SPLIT)" % (split, -(-n_frames // split)) if split > 1 else
-                        "one encode stream and lock per device" if shared else "own streams, concurrent encodes"),
+                        "in frame order; PIXPATH_FFV1_SPLIT forced)" % (split, -(-n_frames // split)) if forced else
+                        "writer_split: %d encoder lanes (sub-batches of %d frames coded side by side, packets written "
+                        "in frame order) for a writer coding alone on the device, one encoder of the whole batch "
+                        "for writers opened while another is open (stages.writer_lanes)"
+                        % (split, -(-n_frames // split))),
             "encoder_pool": {"depth": depth, "created": made, "reserve_s": round(reserve_s, 3),
                              "bytes_per_writer": enc_mem},
             "avi_bytes_per_pvs": size, "compression": round(n1 * frame_bytes(dfmt, dw, dh) / size, 3),

@@ -507,6 +507,26 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
             // through the scalar cache: one exposed scalar-load latency per
             // group, not per row (the ds_reads of a row depend on its base)
             constexpr int G = VT <= 2 ? 8 : VT <= 5 ? 4 : 2;
+            // 8-bit rows: the ordered dither's accumulator inits, once per
+            // chunk.  A wave's rows are y0 + rg + 4k, so y & 7 takes two values
+            // -- row g0 + 4i of a group is phase i & 1 (G is even) -- and the
+            // lane's 4 columns are fixed: the two phases' inits are computed
+            // here instead of a scalar dither load, a 64-bit rotate and 4
+            // byte extracts per row (11 of the 35 VALU of a FUSE-9 row)
+            int dac[2][4];
+            if constexpr (OUTB == 8) {
+#pragma unroll
+                for (int ph = 0; ph < 2; ++ph) {
+                    uint32_t d4 = 0x40404040u;  // flat 64 without dither
+                    if (a.dither) {
+                        const uint64_t rv = as_kconst<uint64_t>(c_dither64)[(y0 + rg + 4 * ph) & 7];
+                        const int rot = ((vxo + J.dither_off) & 7) * 8;
+                        d4 = (uint32_t)(rot ? (rv >> rot) | (rv << (64 - rot)) : rv);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) dac[ph][j] = (int)((d4 >> (8 * j)) & 0xffu) << 12;
+                }
+            }
             for (int g0 = rg; g0 < ny; g0 += 4 * G) {
                 int vb[G];
                 int32_t cf[G][VT];
@@ -529,31 +549,21 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
 #pragma unroll
                     for (int j = 0; j < VT; ++j) q[j] = rp[j * (TW / 4)];
                     int acc[4];
+                    // the first tap pair onto the rounding constant (16-bit rows)
+                    // or the row's dither init (8-bit rows), both VGPRs
                     if constexpr (OUTB == 8) {
-                        // ordered dither: the row's 8 bytes (scalar load, y is wave-uniform)
-                        // rotated to the lane's first column; flat 64 without dither
-                        uint32_t d4 = 0x40404040u;
-                        if (a.dither) {
-                            const uint64_t rv = as_kconst<uint64_t>(c_dither64)[y & 7];
-                            const int rot = ((vxo + J.dither_off) & 7) * 8;
-                            d4 = (uint32_t)(rot ? (rv >> rot) | (rv << (64 - rot)) : rv);
-                        }
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) acc[j] = (int)((d4 >> (8 * j)) & 0xffu) << 12;
+                        acc[0] = dot2_sv(__builtin_bit_cast(v2i16, q[0].x), cf[i][0], dac[i & 1][0]);
+                        acc[1] = dot2_sv(__builtin_bit_cast(v2i16, q[0].y), cf[i][0], dac[i & 1][1]);
+                        acc[2] = dot2_sv(__builtin_bit_cast(v2i16, q[0].z), cf[i][0], dac[i & 1][2]);
+                        acc[3] = dot2_sv(__builtin_bit_cast(v2i16, q[0].w), cf[i][0], dac[i & 1][3]);
                     } else {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) acc[j] = kround;
-                    }
-                    int j0 = 0;
-                    if constexpr (OUTB != 8) {  // first tap pair onto the rounding constant
                         acc[0] = dot2_sv(__builtin_bit_cast(v2i16, q[0].x), cf[i][0], kround);
                         acc[1] = dot2_sv(__builtin_bit_cast(v2i16, q[0].y), cf[i][0], kround);
                         acc[2] = dot2_sv(__builtin_bit_cast(v2i16, q[0].z), cf[i][0], kround);
                         acc[3] = dot2_sv(__builtin_bit_cast(v2i16, q[0].w), cf[i][0], kround);
-                        j0 = 1;
                     }
 #pragma unroll
-                    for (int j = j0; j < VT; ++j) {
+                    for (int j = 1; j < VT; ++j) {
                         const v2i16 c2 = __builtin_bit_cast(v2i16, cf[i][j]);
                         acc[0] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].x), c2, acc[0], false);
                         acc[1] = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, q[j].y), c2, acc[1], false);
@@ -704,6 +714,21 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
                                     acc[j] = (acc2[h][j] << 7) + (OUT2 == 8 ? 64 << 12 : 1 << (10 + 16 - OUT2));
                                 if ((!CL && !lane_any) || r2 >= hi2) continue;
                                 constexpr int s2 = OUT2 == 8 ? 19 : 11 + 16 - OUT2;
+                                if constexpr (OUT2 == 10) {
+                                    if (CL || (lane_full && a.vec_dst)) {
+                                        // (acc2 << 7) + 2^16 >> 17 == (acc2 + 512) >> 10, the high
+                                        // half of 64 (acc2 + 512): one v_lshl_add per output, then
+                                        // both halves' clamp as packed 16-bit ops (clamp_pack16)
+                                        int hv[4];
+#pragma unroll
+                                        for (int j = 0; j < 4; ++j) hv[j] = (acc2[h][j] << 6) + 32768;
+                                        uint2 v;
+                                        v.x = clamp_pack16<16, 1023>(hv[0], hv[1]);
+                                        v.y = clamp_pack16<16, 1023>(hv[2], hv[3]);
+                                        *reinterpret_cast<uint2 *>(dbase + (int64_t)r2 * dls + 2 * vxo) = v;
+                                        continue;
+                                    }
+                                }
                                 int w[4];
 #pragma unroll
                                 for (int j = 0; j < 4; ++j) w[j] = min(max(acc[j] >> s2, 0), (1 << OUT2) - 1);

@@ -242,8 +242,21 @@ def reserve_encoders(fmt, w, h, count, slices=(8, 8), max_frames=600, device=Non
 
 def reserve_writers(fmt, w, h, count, slices=(8, 8), batch=600, device=None, split=None):
     """reserve_encoders for `count` AVPVS writers (Ffv1AviWriter) of `batch`
-    frames with `split` encoder lanes each (default_split()): count x split
-    encoders of ceil(batch / split) frames, one staging batch each."""
+    frames in flight at once.  split = K: count x K encoders of ceil(batch / K)
+    frames, one staging batch each.  split None (the writers' default, see
+    writer_split): the first writer codes alone on the device and takes
+    default_split() lanes, the other count - 1 open while it is still open and
+    take one encoder of the whole batch; PIXPATH_FFV1_SPLIT set forces K for
+    every writer."""
+    made = 0
+    if split is None and not os.environ.get("PIXPATH_FFV1_SPLIT"):
+        k = default_split()
+        made += reserve_encoders(fmt, w, h, k, slices=slices, max_frames=-(-int(batch) // k), device=device,
+                                 stages=1)
+        if count > 1:
+            made += reserve_encoders(fmt, w, h, count - 1, slices=slices, max_frames=int(batch), device=device,
+                                     stages=1)
+        return made
     k = default_split() if split is None else max(1, int(split))
     sub = -(-int(batch) // k)
     return reserve_encoders(fmt, w, h, count * k, slices=slices, max_frames=sub, device=device, stages=1)
@@ -393,7 +406,8 @@ def provenance(slices):
 
 
 def default_split():
-    """Encoders per AVPVS writer (PIXPATH_FFV1_SPLIT, default 2): the 600-frame
+    """Encoders of an AVPVS writer that codes alone on its device (writer_split;
+    PIXPATH_FFV1_SPLIT, default 2, forces it for every writer): the 600-frame
     batch of a PVS is coded as that many sub-batches, each on its own encoder,
     stream and worker thread, so the first half's encode starts while the
     pipeline still scales the second half, the halves code side by side (one
@@ -404,6 +418,26 @@ def default_split():
     if not v.isdigit() or not 1 <= int(v) <= 8:
         raise ValueError("PIXPATH_FFV1_SPLIT must be 1..8")
     return int(v)
+
+
+_OPEN_LOCK = threading.Lock()
+_OPEN = {}  # device -> AVPVS writers open on it
+
+
+def writer_split(device, opened=None):
+    """Encoder lanes for a new AVPVS writer on `device`: PIXPATH_FFV1_SPLIT when
+    set, else default_split() when no other writer is open on the device (one
+    PVS coding alone leaves SIMDs idle, which the lanes fill) and 1 when others
+    are (their encodes fill the device already: on MI355X, 4 PVSes in flight
+    code at 3.0k fps with one encoder each but 2.2-2.5k fps with two lanes each
+    -- 8 encode streams on 4 hardware queues, profiles/r6/ab/README.md).
+    `opened`: writers open on the device (default: the live count)."""
+    if os.environ.get("PIXPATH_FFV1_SPLIT"):
+        return default_split()
+    if opened is None:
+        with _OPEN_LOCK:
+            opened = _OPEN.get(int(device), 0)
+    return default_split() if opened == 0 else 1
 
 
 class Ffv1AviWriter:
@@ -418,7 +452,8 @@ class Ffv1AviWriter:
     is encoded by a worker thread on its own stream while the next batch fills
     (a second staging batch, allocated only when a PVS has more than one
     batch), its packets come back in one pinned D2H and go into the AVI.  With
-    ``split`` = K > 1 (the default, default_split) the batch is K sub-batches
+    ``split`` = K > 1 (writer_split: 2 when the writer codes alone on the
+    device) the batch is K sub-batches
     on K encoder LANES -- each lane its own encoder, staging batch, streams and
     worker thread -- submitted as each fills: the lanes' encodes overlap the
     pipeline and each other, and a lane writes its packets as soon as the
@@ -431,15 +466,16 @@ class Ffv1AviWriter:
         shared (split = 1 only): encode on the device's shared stream under
         its encode lock (_device_state); False gives the writer its own
         streams and lets its encodes overlap other writers' (bench comparison
-        only).  split: encoder lanes (default_split())."""
+        only).  split: encoder lanes (default writer_split(device))."""
         import time
         from . import avi
         t0 = time.perf_counter()
         if slices is None:
             slices = default_slices()
-        if split is None:
-            split = default_split()
         self.fmt = formats.fmt(fmt)
+        self._open_dev = None
+        if split is None:
+            split = writer_split(context(device).device)
         self.w, self.h = int(w), int(h)
         self.fb = formats.frame_bytes(self.fmt, w, h)
         self.batch = int(batch)
@@ -486,6 +522,9 @@ class Ffv1AviWriter:
         self.ths = [threading.Thread(target=self._work, args=(k,), daemon=True) for k in range(self.K)]
         for t in self.ths:
             t.start()
+        with _OPEN_LOCK:  # counted open until close(): writers made meanwhile take one lane
+            self._open_dev = self.device.index
+            _OPEN[self._open_dev] = _OPEN.get(self._open_dev, 0) + 1
 
     def _stage(self, slot):
         from .frames import FrameBatch
@@ -674,6 +713,13 @@ class Ffv1AviWriter:
                 except Exception:
                     pass
             self.release(ok)
+            self._closed()
+
+    def _closed(self):
+        dev, self._open_dev = self._open_dev, None
+        if dev is not None:
+            with _OPEN_LOCK:
+                _OPEN[dev] = max(0, _OPEN.get(dev, 0) - 1)
 
 
 class Ffv1AviReader:

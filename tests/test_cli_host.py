@@ -291,3 +291,19 @@ def test_decoder_route_by_stream_shape(monkeypatch):
     monkeypatch.setenv("PIXPATH_FFV1", "ffmpeg")
     assert ffv1.decoder_route(gops, have_ffmpeg=False) == "ffmpeg"
     assert ffv1.decoder_route(own, have_ffmpeg=False) == "gpu"
+
+
+def test_writer_split_by_open_writers(monkeypatch):
+    """writer_split (the AVPVS writer's encoder lanes): default_split() lanes
+    for a writer coding alone on its device, one encoder when other writers
+    are open there; PIXPATH_FFV1_SPLIT forces the count for every writer and
+    is range-checked."""
+    from pixpath import ffv1
+    monkeypatch.delenv("PIXPATH_FFV1_SPLIT", raising=False)
+    assert ffv1.writer_split(0, opened=0) == 2
+    assert ffv1.writer_split(0, opened=3) == 1
+    monkeypatch.setenv("PIXPATH_FFV1_SPLIT", "3")
+    assert ffv1.writer_split(0, opened=0) == 3 and ffv1.writer_split(0, opened=2) == 3
+    monkeypatch.setenv("PIXPATH_FFV1_SPLIT", "9")
+    with pytest.raises(ValueError):
+        ffv1.writer_split(0, opened=0)

@@ -394,6 +394,24 @@ def test_writer_lanes_write_the_same_file(gpu, tmp_path, split):
             np.testing.assert_array_equal(dec[p], frames[i][p], err_msg="frame %d plane %d" % (i, p))
 
 
+def test_writer_lanes_by_open_writers(gpu, tmp_path, monkeypatch):
+    """writer_split: a writer opened alone on the device takes default_split()
+    lanes, one opened while it is open takes one encoder of the whole batch,
+    and once both are closed the next writer takes lanes again."""
+    from pixpath import ffv1
+    monkeypatch.delenv("PIXPATH_FFV1_SPLIT", raising=False)
+    mk = lambda name: ffv1.Ffv1AviWriter(str(tmp_path / name), "yuv422p10le", 64, 32, 60, slices=(1, 1),
+                                         batch=6, device=gpu)
+    a = mk("a.avi")
+    b = mk("b.avi")
+    assert a.K == ffv1.default_split() == 2 and b.K == 1 and b.sub == 6 and a.sub == 3
+    b.close()
+    a.close()
+    c = mk("c.avi")
+    assert c.K == 2
+    c.close()
+
+
 def test_record_budget_split_keeps_the_bytes(gpu):
     """The per-slice renorm-record budget (pp_ffv1_encode_packets): a batch of
     mostly smooth frames with noise frames among them overflows the budget
