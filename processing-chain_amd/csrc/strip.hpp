@@ -513,8 +513,11 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
             // lane's 4 columns are fixed: the two phases' inits are computed
             // here instead of a scalar dither load, a 64-bit rotate and 4
             // byte extracts per row (11 of the 35 VALU of a FUSE-9 row)
+            // (config 4's 10-bit-source instances only: the 8-VGPR table spills
+            // the other 8-bit-output instances at their register budgets)
+            constexpr bool DACPRE = OUTB == 8 && sizeof(ST) == 2 && (FUSE == 9 || FUSE == 11);
             int dac[2][4];
-            if constexpr (OUTB == 8) {
+            if constexpr (DACPRE) {
 #pragma unroll
                 for (int ph = 0; ph < 2; ++ph) {
                     uint32_t d4 = 0x40404040u;  // flat 64 without dither
@@ -551,7 +554,23 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
                     int acc[4];
                     // the first tap pair onto the rounding constant (16-bit rows)
                     // or the row's dither init (8-bit rows), both VGPRs
-                    if constexpr (OUTB == 8) {
+                    if constexpr (OUTB == 8 && !DACPRE) {
+                        // ordered dither: the row's 8 bytes (scalar load, y is wave-uniform)
+                        // rotated to the lane's first column; flat 64 without dither
+                        uint32_t d4 = 0x40404040u;
+                        if (a.dither) {
+                            const uint64_t rv = as_kconst<uint64_t>(c_dither64)[y & 7];
+                            const int rot = ((vxo + J.dither_off) & 7) * 8;
+                            d4 = (uint32_t)(rot ? (rv >> rot) | (rv << (64 - rot)) : rv);
+                        }
+                        int dj[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) dj[j] = (int)((d4 >> (8 * j)) & 0xffu) << 12;
+                        acc[0] = dot2_sv(__builtin_bit_cast(v2i16, q[0].x), cf[i][0], dj[0]);
+                        acc[1] = dot2_sv(__builtin_bit_cast(v2i16, q[0].y), cf[i][0], dj[1]);
+                        acc[2] = dot2_sv(__builtin_bit_cast(v2i16, q[0].z), cf[i][0], dj[2]);
+                        acc[3] = dot2_sv(__builtin_bit_cast(v2i16, q[0].w), cf[i][0], dj[3]);
+                    } else if constexpr (OUTB == 8) {
                         acc[0] = dot2_sv(__builtin_bit_cast(v2i16, q[0].x), cf[i][0], dac[i & 1][0]);
                         acc[1] = dot2_sv(__builtin_bit_cast(v2i16, q[0].y), cf[i][0], dac[i & 1][1]);
                         acc[2] = dot2_sv(__builtin_bit_cast(v2i16, q[0].z), cf[i][0], dac[i & 1][2]);
@@ -714,7 +733,7 @@ __global__ __launch_bounds__(TW, (FUSE >= 8 ? strip_fused_min_waves<HW, VTM, FUS
                                     acc[j] = (acc2[h][j] << 7) + (OUT2 == 8 ? 64 << 12 : 1 << (10 + 16 - OUT2));
                                 if ((!CL && !lane_any) || r2 >= hi2) continue;
                                 constexpr int s2 = OUT2 == 8 ? 19 : 11 + 16 - OUT2;
-                                if constexpr (OUT2 == 10) {
+                                if constexpr (FUSE == 11) {  // (FUSE 10 spills with it)
                                     if (CL || (lane_full && a.vec_dst)) {
                                         // (acc2 << 7) + 2^16 >> 17 == (acc2 + 512) >> 10, the high
                                         // half of 64 (acc2 + 512): one v_lshl_add per output, then
