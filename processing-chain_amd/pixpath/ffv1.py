@@ -498,6 +498,7 @@ class Ffv1AviWriter:
             e.set()
         self.cur, self.fill = 0, 0
         self.free[0].clear()
+        self.claimed = True  # slot 0 is this writer's from the start
         if shared and self.K == 1:
             lock, st, self.put_stream, d2h = _device_state(self.device.index)
             self.lanes = [(lock, st, d2h)]
@@ -620,15 +621,25 @@ class Ffv1AviWriter:
         self.qs[self.lane_of[self.cur]].put((self.cur, self.fill, ev, time.perf_counter(), self.seq))
         self.seq += 1
         self.cur = (self.cur + 1) % self.nslots
-        self.free[self.cur].wait()
-        self.free[self.cur].clear()
+        # the next slot is claimed when its first frames arrive (_claim), not
+        # here: after a batch's last sub-batch the caller goes on (the next
+        # PVS's pipeline) instead of waiting for lane 0's encode to free it
+        self.claimed = False
         self.fill = 0
         self._check()
+
+    def _claim(self):
+        if not self.claimed:
+            self.free[self.cur].wait()
+            self.free[self.cur].clear()
+            self.claimed = True
+            self._check()
 
     def _put(self, rows, stream):
         """Append device frames (uint8 rows [k, frame_bytes]) on `stream`."""
         k, i = rows.shape[0], 0
         while i < k:
+            self._claim()
             take = min(k - i, self.sub - self.fill)
             stage = self._stage(self.cur)
             with torch.cuda.stream(stream):
