@@ -566,7 +566,12 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None, shared=True):
         n1, dt1, w1 = min(singles, key=lambda r: r[1])
         single_runs = [round(r[1], 3) for r in singles]
         size = w1["avi_bytes"]
-        n, dt, ws = run(n_pvs)
+        # the PVSes in flight: the best of 2 runs (their host stages -- frames
+        # into pinned batches, packet D2H and AVI writes -- contend for host
+        # memory and vary run to run; both runs' seconds are reported)
+        multi = [run(n_pvs) for _ in range(2)]
+        n, dt, ws = min(multi, key=lambda r: r[1])
+        multi_runs = [round(r[1], 3) for r in multi]
     finally:
         for f in os.listdir(d):
             os.remove(os.path.join(d, f))
@@ -580,7 +585,8 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None, shared=True):
         except Exception:
             pass
     ffv1.clear_pool()
-    return {"frames_per_s": round(n / dt, 1), "frames": n, "pvs": n_pvs, "seconds": round(dt, 3), "stages": ws,
+    return {"frames_per_s": round(n / dt, 1), "frames": n, "pvs": n_pvs, "seconds": round(dt, 3), "runs_s": multi_runs,
+            "stages": ws,
             "single_pvs": {"frames_per_s": round(n1 / dt1, 1), "seconds": round(dt1, 3), "runs_s": single_runs,
                            "stages": w1},
             "writers": ("%d encoder lanes per writer (sub-batches of %d frames coded side by side, packets written "
@@ -596,7 +602,8 @@ def e2e_avpvs(wl, n_frames, dev, n_pvs=4, depth=None, shared=True):
                     "(720p->1080p yuv422p10le lanczos) -> FFV1 v3 encode on the device output (8x8 slices, the "
                     "writer's encoder lanes: worker threads and streams) -> packets D2H -> AVI file; consecutive "
                     "PVSes overlap; %d pooled encoders reserved before timing; decode of the SRC bitstream "
-                    "excluded (ffmpeg is absent on the box)" % (n_pvs, n_frames, depth)}
+                    "excluded (ffmpeg is absent on the box); frames_per_s: the best of 2 runs of the %d PVSes "
+                    "(runs_s), single_pvs: the best of 3" % (n_pvs, n_frames, depth, n_pvs)}
 
 
 def make_inputs(wl, n, seed, dev):
